@@ -1,0 +1,128 @@
+"""ctypes binding of libaudiolcm_hip.so (the C-ABI declared in include/audiolcm_hip.h).
+
+The library is built in-tree (``audiolcm_amd/libaudiolcm_hip.so``) by
+``__graft_entry__.build()`` / ``make -C audiolcm_amd/csrc``.  There is no
+fallback: if the library is missing or the device is not gfx950 every call
+raises, so a GPU run can never silently take a CPU or eager-PyTorch path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ALCM_LIB", os.path.join(HERE, "libaudiolcm_hip.so"))
+
+ALCM_OPND_ACT, ALCM_OPND_ACT_T, ALCM_OPND_WEIGHT = 0, 1, 2
+ALCM_MODEL_DIT, ALCM_MODEL_VAE, ALCM_MODEL_BIGVGAN = 0, 1, 2
+ACT_NONE, ACT_SILU, ACT_GELU_ERF, ACT_GELU_TANH, ACT_TANH = 0, 1, 2, 3, 4
+
+i64 = C.c_int64
+vp = C.c_void_p
+fp = C.c_void_p  # float* passed as raw device address
+
+
+class Operand(C.Structure):
+    _fields_ = [("kind", C.c_int), ("ptr", vp), ("sb", i64), ("st", i64), ("sc", i64),
+                ("T_in", C.c_int), ("C_in", C.c_int), ("Cpad", C.c_int), ("ksize", C.c_int), ("dil", C.c_int),
+                ("pad", C.c_int), ("up", C.c_int), ("rows_per_batch", C.c_int), ("rows", C.c_int),
+                ("zs1", i64), ("zs2", i64), ("pro_scale", fp), ("pro_shift", fp), ("pro_sb", i64),
+                ("pro_mean", fp), ("pro_rstd", fp), ("pro_act", C.c_int), ("w_lo_off", i64)]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("Kpad", C.c_int), ("batch", C.c_int), ("zdiv", C.c_int),
+                ("a", Operand), ("b", Operand), ("bias", fp), ("acc_scale", C.c_float), ("out_scale", C.c_float),
+                ("act", C.c_int), ("accumulate", C.c_int), ("geglu", C.c_int), ("res", fp),
+                ("r_sb", i64), ("r_st", i64), ("r_sc", i64), ("r_zs1", i64), ("r_zs2", i64), ("out", fp),
+                ("o_sb", i64), ("o_st", i64), ("o_sc", i64), ("o_zs1", i64), ("o_zs2", i64),
+                ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("split", C.c_int)]
+
+
+class NamedTensor(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data", vp), ("ndim", C.c_int), ("shape", i64 * 4)]
+
+
+# (name, restype, argtypes) — every symbol include/audiolcm_hip.h declares
+_SIGS = [
+    ("alcm_last_error", C.c_char_p, []),
+    ("alcm_version", C.c_int, []),
+    ("alcm_check_device", C.c_int, [C.c_int]),
+    ("alcm_gemm", C.c_int, [C.POINTER(GemmArgs), vp]),
+    ("alcm_pack_conv_weight", C.c_int, [fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        vp, vp]),
+    ("alcm_group_norm_affine", C.c_int, [fp, C.c_int, C.c_int, C.c_int, i64, i64, C.c_int, C.c_float, fp, fp, fp,
+                                         fp, vp]),
+    ("alcm_row_stats", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, vp]),
+    ("alcm_layer_norm", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, fp, i64, fp, i64, vp]),
+    ("alcm_softmax_rows", C.c_int, [fp, C.c_int, C.c_int, i64, vp]),
+    ("alcm_activation1d", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, i64, i64, fp, fp, fp, fp, vp]),
+    ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
+    ("alcm_lcm_step_cfg", C.c_int, [fp, fp, fp, C.c_float, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
+    ("alcm_sincos_embedding", C.c_int, [fp, C.c_float, fp, C.c_int, C.c_int, C.c_int, fp, vp]),
+    ("alcm_model_create", C.c_int, [C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(NamedTensor), C.c_int, C.c_int,
+                                    C.POINTER(vp)]),
+    ("alcm_model_destroy", C.c_int, [vp]),
+    ("alcm_model_weight_bytes", C.c_size_t, [vp]),
+    ("alcm_model_set_split", C.c_int, [vp, C.c_int]),
+    ("alcm_dit_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
+    ("alcm_dit_embed_context", C.c_int, [vp, fp, C.c_int, fp, vp, C.c_size_t, vp]),
+    ("alcm_dit_forward", C.c_int, [vp, fp, vp, fp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+    ("alcm_vae_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
+    ("alcm_vae_decode", C.c_int, [vp, fp, C.c_float, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+    ("alcm_bigvgan_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
+    ("alcm_bigvgan_forward", C.c_int, [vp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+]
+EXPORTED = [s[0] for s in _SIGS]
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """Load the HIP library (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libaudiolcm_hip.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                              "(make -C audiolcm_amd/csrc). The MI355X path has no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().alcm_last_error().decode(errors="replace")
+        raise HipError(f"{what or 'alcm call'} failed ({rc}): {msg}")
+
+
+_checked_devices = set()
+
+
+def require_device(dev: int = 0) -> None:
+    if dev in _checked_devices:
+        return
+    check(lib().alcm_check_device(dev), "alcm_check_device")
+    _checked_devices.add(dev)
+
+
+def stream_handle(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t) -> Optional[int]:
+    """Device address of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return int(t.data_ptr())

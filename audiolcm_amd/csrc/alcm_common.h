@@ -1,0 +1,77 @@
+// Shared device/host helpers for the AudioLCM MI355X (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ALCM_WAVE 64
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+// Magic-number unsigned division for n, d < 2^31 (row -> (batch, time) decode).
+struct FastDiv {
+  uint32_t d, m, s;
+  __host__ __device__ FastDiv() : d(1), m(1), s(0) {}
+  __host__ FastDiv(uint32_t dv) : d(dv ? dv : 1) {
+    s = 0;
+    while ((1u << s) < d) ++s;
+    m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    uint32_t t = __umulhi(n, m);
+    return (t + n) >> s;
+  }
+  __device__ __forceinline__ void divmod(uint32_t n, uint32_t& q, uint32_t& r) const {
+    q = div(n);
+    r = n - q * d;
+  }
+};
+
+// Activation codes shared by GEMM prologue/epilogue and elementwise kernels.
+enum AlcmAct : int {
+  ACT_NONE = 0,
+  ACT_SILU = 1,       // x * sigmoid(x)  (nn.SiLU / VAE swish)
+  ACT_GELU_ERF = 2,   // F.gelu default
+  ACT_GELU_TANH = 3,  // F.gelu(approximate='tanh')
+  ACT_TANH = 4,
+};
+
+__device__ __forceinline__ float alcm_act(float x, int act) {
+  switch (act) {
+    case ACT_SILU: return x / (1.0f + expf(-x));
+    case ACT_GELU_ERF: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    case ACT_GELU_TANH: {
+      const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+      float u = k0 * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.0f + tanhf(u));
+    }
+    case ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Host-side round-to-nearest-even fp32 -> bf16 bits (weights only; no NaN handling needed).
+static inline u16 host_bf16_bits(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+static inline float host_bf16_to_f32(u16 b) {
+  uint32_t u = ((uint32_t)b) << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}

@@ -1,0 +1,538 @@
+// MFMA implicit-GEMM for every contraction on the AudioLCM hot path (gfx950 / CDNA4).
+//
+//   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] )
+//
+// One kernel template covers: conv1d of any kernel size / dilation / zero padding
+// (implicit GEMM, K = tap*Cpad + ci), nearest-x2 upsample folded into the input index
+// (Upsample1D, autoencoder1d.py:280-295), ConvTranspose1d as per-phase convolutions
+// (BigVGAN ups, models.py:160-165), Linear layers, and the batched attention products
+// Q K^T and P V (new_attention.py:114-126, autoencoder1d.py:265-274).
+//
+// Activations are fp32, channels-last (b, t, c) in HBM; operands are rounded to bf16 while
+// they are staged into LDS and fed to v_mfma_f32_16x16x32_bf16 with fp32 accumulate.  With
+// SPLIT each fp32 operand is carried as hi = bf16(x), lo = bf16(x - hi) and the product is
+// hi*hi + hi*lo + lo*hi (3 MFMAs): ~2^-16 relative error, i.e. fp32-reference parity at 3x
+// the bf16 MFMA cost (still 5.3x the f32-input MFMA rate).
+//
+// Prologue (A operand, applied on load): GroupNorm/LayerNorm affine + SiLU, so norm+act+conv
+// is one pass over HBM.  Epilogue: bias, acc scale, activation, GEGLU pair gating
+// (new_attention.py:48-55), residual add, output scale, accumulate (BigVGAN mean of
+// resblocks, models.py:193-199), strided store (channels-last or NCT, conv-transpose phases).
+#include "alcm_common.h"
+#include "audiolcm_hip.h"
+#include "alcm_internal.h"
+
+namespace alcm {
+
+constexpr int BK = 32;
+constexpr int LDS_ROW = 40;  // bf16 per LDS row: 32 + 8 pad (80 B) -> ds_read_b128 aligned, fewer conflicts
+
+struct ActDev {
+  const float* p;
+  int64_t sb, st, sc;
+  int T_in, C_in, Cpad, ksize, dil, pad, up, Kreal, M;
+  FastDiv rpb, cpad;
+  int64_t zs1, zs2;
+  const float* ps;
+  const float* ph;
+  int64_t psb;
+  const float* pm;
+  const float* pr;
+  int pact;
+};
+struct ActTDev {
+  const float* p;
+  int64_t st, sc;
+  int Kext, rows;
+  int64_t zs1, zs2;
+};
+struct WDev {
+  const u16* p;
+  int64_t lo;
+  int rows, Kpad;
+};
+struct EpiDev {
+  const float* bias;
+  float acc_scale, out_scale;
+  int act, accumulate, geglu;
+  const float* res;
+  int64_t r_sb, r_st, r_sc, r_zs1, r_zs2;
+  float* out;
+  int64_t o_sb, o_st, o_sc, o_zs1, o_zs2;
+  FastDiv orpb;
+  int out_step, out_off;
+};
+struct GemmDev {
+  int M, N, Kpad;
+  FastDiv zdiv;
+  ActDev a;
+  ActDev bact;
+  ActTDev bT;
+  WDev w;
+  EpiDev e;
+};
+
+enum { BK_W = 0, BK_ACT = 1, BK_ACTT = 2 };
+
+__device__ __forceinline__ int64_t zoff(const FastDiv& zd, int z, int64_t s1, int64_t s2) {
+  uint32_t q, r;
+  zd.divmod((uint32_t)z, q, r);
+  return (int64_t)q * s1 + (int64_t)r * s2;
+}
+
+__device__ __forceinline__ void split_store(const float (&v)[8], __bf16* hi, __bf16* lo, bool split) {
+  bf16x8 h, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 bh = (__bf16)v[j];
+    h[j] = bh;
+    if (split) l[j] = (__bf16)(v[j] - (float)bh);
+  }
+  *reinterpret_cast<bf16x8*>(hi) = h;
+  if (split) *reinterpret_cast<bf16x8*>(lo) = l;
+}
+
+// ---------------------------------------------------------------- fp32 activation tile (conv taps)
+template <int ROWS, bool VEC>
+struct ActTile {
+  static constexpr int CHUNKS = ROWS * 4;
+  static constexpr int PER = (CHUNKS + 255) / 256;
+  const float* base[PER];
+  int t[PER];
+  int b[PER];
+  bool ok[PER];
+  float v[PER][8];
+
+  __device__ __forceinline__ void init(const ActDev& A, int tid, int row0, int64_t zo) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      const int r = row0 + (c >> 2);
+      ok[i] = (c < CHUNKS) && (r < A.M);
+      uint32_t bb = 0, tt = 0;
+      if (ok[i]) A.rpb.divmod((uint32_t)r, bb, tt);
+      b[i] = (int)bb;
+      t[i] = (int)tt;
+      base[i] = A.p + zo + (int64_t)bb * A.sb;
+    }
+  }
+  __device__ __forceinline__ void load(const ActDev& A, int tid, int k0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      const int c = tid + i * 256;
+      const int k = k0 + (c & 3) * 8;
+      if (!ok[i] || k >= A.Kreal) continue;
+      const int tap = (int)A.cpad.div((uint32_t)k);
+      const int ci = k - tap * A.Cpad;
+      int ts = t[i] + tap * A.dil - A.pad;
+      if (A.up == 2) {
+        if (ts < 0 || ts >= 2 * A.T_in) continue;
+        ts >>= 1;
+      } else if (ts < 0 || ts >= A.T_in) {
+        continue;
+      }
+      const float* src = base[i] + (int64_t)ts * A.st;
+      if (VEC) {
+        const float4 x0 = *reinterpret_cast<const float4*>(src + ci);
+        const float4 x1 = *reinterpret_cast<const float4*>(src + ci + 4);
+        v[i][0] = x0.x; v[i][1] = x0.y; v[i][2] = x0.z; v[i][3] = x0.w;
+        v[i][4] = x1.x; v[i][5] = x1.y; v[i][6] = x1.z; v[i][7] = x1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (ci + j < A.C_in) v[i][j] = src[(int64_t)(ci + j) * A.sc];
+      }
+      if (A.pm) {
+        const int64_t ri = (int64_t)b[i] * A.T_in + ts;
+        const float mu = A.pm[ri], rs = A.pr[ri];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mu) * rs;
+      }
+      if (A.ps) {
+        const float* sc = A.ps + (int64_t)b[i] * A.psb + ci;
+        const float* sh = A.ph + (int64_t)b[i] * A.psb + ci;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (VEC || ci + j < A.C_in) v[i][j] = v[i][j] * sc[j] + sh[j];
+      }
+      if (A.pact) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (VEC || ci + j < A.C_in) v[i][j] = alcm_act(v[i][j], A.pact);
+      }
+    }
+  }
+  template <bool SPLIT>
+  __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      if (c >= CHUNKS) continue;
+      const int off = (c >> 2) * LDS_ROW + (c & 3) * 8;
+      split_store(v[i], hi + off, lo + off, SPLIT);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- fp32 N-contiguous tile (P V's V operand)
+template <int ROWS>
+struct ActTTile {
+  static constexpr int CHUNKS = ROWS * 4;
+  static constexpr int PER = (CHUNKS + 255) / 256;
+  const float* base;
+  float v[PER][8];
+  __device__ __forceinline__ void init(const ActTDev& B, int tid, int row0, int64_t zo) { base = B.p + zo; }
+  __device__ __forceinline__ void load(const ActTDev& B, int tid, int row0, int k0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      const int n = row0 + (c % ROWS);
+      const int kk = k0 + (c / ROWS) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = (c < CHUNKS) && (n < B.rows) && (kk + j < B.Kext);
+        v[i][j] = ok ? base[(int64_t)(kk + j) * B.st + (int64_t)n * B.sc] : 0.f;
+      }
+    }
+  }
+  template <bool SPLIT>
+  __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      if (c >= CHUNKS) continue;
+      const int off = (c % ROWS) * LDS_ROW + (c / ROWS) * 8;
+      split_store(v[i], hi + off, lo + off, SPLIT);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- packed bf16 weight tile
+template <int ROWS>
+struct WTile {
+  static constexpr int CHUNKS = ROWS * 4;
+  static constexpr int PER = (CHUNKS + 255) / 256;
+  uint4 h[PER], l[PER];
+  __device__ __forceinline__ void load(const WDev& W, int tid, int row0, int k0, bool split) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      const int r = row0 + (c >> 2);
+      h[i] = make_uint4(0, 0, 0, 0);
+      l[i] = make_uint4(0, 0, 0, 0);
+      if (c < CHUNKS && r < W.rows) {
+        const u16* src = W.p + (int64_t)r * W.Kpad + k0 + (c & 3) * 8;
+        h[i] = *reinterpret_cast<const uint4*>(src);
+        if (split) l[i] = *reinterpret_cast<const uint4*>(src + W.lo);
+      }
+    }
+  }
+  template <bool SPLIT>
+  __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 256;
+      if (c >= CHUNKS) continue;
+      const int off = (c >> 2) * LDS_ROW + (c & 3) * 8;
+      *reinterpret_cast<uint4*>(hi + off) = h[i];
+      if (SPLIT) *reinterpret_cast<uint4*>(lo + off) = l[i];
+    }
+  }
+};
+
+// ---------------------------------------------------------------- the kernel
+template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, bool SPLIT>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
+  constexpr int TM = BM / (WM * 16);
+  constexpr int TN = BN / (WN * 16);
+  constexpr int NP = SPLIT ? 2 : 1;
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][NP][BM * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][NP][BN * LDS_ROW];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int row0 = blockIdx.x * BM;
+  const int col0 = blockIdx.y * BN;
+  const int z = blockIdx.z;
+
+  ActTile<BM, AVEC> at;
+  at.init(P.a, tid, row0, zoff(P.zdiv, z, P.a.zs1, P.a.zs2));
+  ActTile<BN, true> bt_act;
+  ActTTile<BN> bt_t;
+  WTile<BN> bt_w;
+  if constexpr (BKIND == BK_ACT) bt_act.init(P.bact, tid, col0, zoff(P.zdiv, z, P.bact.zs1, P.bact.zs2));
+  if constexpr (BKIND == BK_ACTT) bt_t.init(P.bT, tid, col0, zoff(P.zdiv, z, P.bT.zs1, P.bT.zs2));
+
+  auto load_tiles = [&](int k0) {
+    at.load(P.a, tid, k0);
+    if constexpr (BKIND == BK_W) bt_w.load(P.w, tid, col0, k0, SPLIT);
+    if constexpr (BKIND == BK_ACT) bt_act.load(P.bact, tid, k0);
+    if constexpr (BKIND == BK_ACTT) bt_t.load(P.bT, tid, col0, k0);
+  };
+  auto store_tiles = [&](int buf) {
+    at.template store<SPLIT>(As[buf][0], As[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_W) bt_w.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_ACT) bt_act.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_ACTT) bt_t.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = P.Kpad / BK;
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+
+  const int a_off = (wm * TM * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
+  const int b_off = (wn * TN * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
+
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nk) load_tiles((ks + 1) * BK);
+
+    bf16x8 ah[TM], bh[TN];
+    bf16x8 al[SPLIT ? TM : 1], bl[SPLIT ? TN : 1];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(&As[cur][0][a_off + i * 16 * LDS_ROW]);
+      if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(&As[cur][NP - 1][a_off + i * 16 * LDS_ROW]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][0][b_off + j * 16 * LDS_ROW]);
+      if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][NP - 1][b_off + j * 16 * LDS_ROW]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (SPLIT) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+
+    if (ks + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const EpiDev& E = P.e;
+  const int64_t ozo = zoff(P.zdiv, z, E.o_zs1, E.o_zs2);
+  const int64_t rzo = E.res ? zoff(P.zdiv, z, E.r_zs1, E.r_zs2) : 0;
+#pragma clang loop unroll(full)
+  for (int i = 0; i < TM; ++i) {
+#pragma clang loop unroll(full)
+    for (int r = 0; r < 4; ++r) {
+      const int m = row0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+      const bool mok = m < P.M;
+      uint32_t bb = 0, tt = 0;
+      if (mok) E.orpb.divmod((uint32_t)m, bb, tt);
+      const int64_t to = (int64_t)tt * E.out_step + E.out_off;
+      const int64_t obase = ozo + (int64_t)bb * E.o_sb + to * E.o_st;
+      const int64_t rbase = rzo + (int64_t)bb * E.r_sb + to * E.r_st;
+#pragma clang loop unroll(full)
+      for (int j = 0; j < TN; ++j) {
+        const int n = col0 + wn * TN * 16 + j * 16 + (lane & 15);
+        float v = acc[i][j][r] * E.acc_scale;
+        if (E.bias && n < P.N) v += E.bias[n];
+        int nout = n;
+        bool st = mok && n < P.N;
+        if (E.geglu) {
+          const float g = __shfl_xor(v, 1);
+          v = v * alcm_act(g, ACT_GELU_ERF);
+          st = st && ((lane & 1) == 0);
+          nout = n >> 1;
+        } else if (E.act) {
+          v = alcm_act(v, E.act);
+        }
+        if (st) {
+          if (E.res) v += E.res[rbase + (int64_t)nout * E.r_sc];
+          v *= E.out_scale;
+          float* o = E.out + obase + (int64_t)nout * E.o_sc;
+          if (E.accumulate) v += *o;
+          *o = v;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host side
+static bool fill_act(const alcm_operand& o, int M, ActDev& d, std::string& err) {
+  d.p = (const float*)o.ptr;
+  d.sb = o.sb; d.st = o.st; d.sc = o.sc;
+  d.T_in = o.T_in; d.C_in = o.C_in; d.Cpad = o.Cpad; d.ksize = o.ksize; d.dil = o.dil;
+  d.pad = o.pad; d.up = o.up ? o.up : 1;
+  d.Kreal = o.ksize * o.Cpad;
+  d.M = M;
+  d.rpb = FastDiv((uint32_t)(o.rows_per_batch > 0 ? o.rows_per_batch : 1));
+  d.cpad = FastDiv((uint32_t)(o.Cpad > 0 ? o.Cpad : 1));
+  d.zs1 = o.zs1; d.zs2 = o.zs2;
+  d.ps = o.pro_scale; d.ph = o.pro_shift; d.psb = o.pro_sb;
+  d.pm = o.pro_mean; d.pr = o.pro_rstd; d.pact = o.pro_act;
+  if (!o.ptr || o.Cpad <= 0 || o.Cpad % 8 || o.C_in > o.Cpad || o.ksize <= 0 || o.T_in <= 0 ||
+      (d.up != 1 && d.up != 2) || o.rows_per_batch <= 0) {
+    err = "bad ACT operand geometry";
+    return false;
+  }
+  if ((o.pro_scale == nullptr) != (o.pro_shift == nullptr) || (o.pro_mean == nullptr) != (o.pro_rstd == nullptr)) {
+    err = "prologue scale/shift and mean/rstd must come in pairs";
+    return false;
+  }
+  return true;
+}
+
+static bool act_vec_ok(const alcm_operand& o) {
+  const bool al = (((uintptr_t)o.ptr) & 15) == 0;
+  return al && o.sc == 1 && o.C_in == o.Cpad && o.Cpad % 8 == 0 && o.st % 4 == 0 && o.sb % 4 == 0 &&
+         o.zs1 % 4 == 0 && o.zs2 % 4 == 0;
+}
+
+template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, bool SPLIT>
+static void launch_one(const GemmDev& P, int batch, int ncols, hipStream_t s) {
+  dim3 grid((P.M + BM - 1) / BM, (ncols + BN - 1) / BN, batch);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AVEC, BKIND, SPLIT>), grid, dim3(256), 0, s, P);
+}
+
+template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND>
+static void launch_split(const GemmDev& P, int batch, int ncols, bool split, hipStream_t s) {
+  if (split) launch_one<BM, BN, WM, WN, AVEC, BKIND, true>(P, batch, ncols, s);
+  else launch_one<BM, BN, WM, WN, AVEC, BKIND, false>(P, batch, ncols, s);
+}
+
+int gemm(const alcm_gemm_args& g, hipStream_t s) {
+  std::string err;
+  if (g.M <= 0 || g.N <= 0) return 0;
+  if (g.Kpad <= 0 || g.Kpad % BK) return set_error(ALCM_E_INVALID, "Kpad must be a positive multiple of 32");
+  if (g.a.kind != ALCM_OPND_ACT) return set_error(ALCM_E_INVALID, "A operand must be ACT");
+  if (!g.out) return set_error(ALCM_E_INVALID, "null output");
+  if (g.geglu && (g.N % 2)) return set_error(ALCM_E_INVALID, "geglu needs even N");
+  GemmDev P{};
+  P.M = g.M; P.N = g.N; P.Kpad = g.Kpad;
+  const int batch = g.batch > 0 ? g.batch : 1;
+  P.zdiv = FastDiv((uint32_t)(g.zdiv > 0 ? g.zdiv : 1));
+  if (!fill_act(g.a, g.M, P.a, err)) return set_error(ALCM_E_INVALID, "A: " + err);
+  if (P.a.Kreal > g.Kpad) return set_error(ALCM_E_INVALID, "Kpad smaller than ksize*Cpad of A");
+  int bkind;
+  if (g.b.kind == ALCM_OPND_WEIGHT) {
+    bkind = BK_W;
+    P.w.p = (const u16*)g.b.ptr; P.w.lo = g.b.w_lo_off; P.w.rows = g.b.rows; P.w.Kpad = g.Kpad;
+    if (!g.b.ptr || g.b.rows < g.N) return set_error(ALCM_E_INVALID, "weight operand rows < N");
+    if ((((uintptr_t)g.b.ptr) & 15) || (g.b.w_lo_off % 8)) return set_error(ALCM_E_INVALID, "weight alignment");
+  } else if (g.b.kind == ALCM_OPND_ACT) {
+    bkind = BK_ACT;
+    if (!fill_act(g.b, g.N, P.bact, err)) return set_error(ALCM_E_INVALID, "B: " + err);
+    if (!act_vec_ok(g.b) || g.b.ksize != 1 || g.b.pro_scale || g.b.pro_mean)
+      return set_error(ALCM_E_INVALID, "B ACT operand must be channel-contiguous, 16B aligned, k=1, no prologue");
+    if (P.bact.Kreal > g.Kpad) return set_error(ALCM_E_INVALID, "Kpad smaller than B K");
+  } else if (g.b.kind == ALCM_OPND_ACT_T) {
+    bkind = BK_ACTT;
+    P.bT.p = (const float*)g.b.ptr; P.bT.st = g.b.st; P.bT.sc = g.b.sc; P.bT.Kext = g.b.T_in;
+    P.bT.rows = g.b.rows; P.bT.zs1 = g.b.zs1; P.bT.zs2 = g.b.zs2;
+    if (!g.b.ptr || g.b.rows < g.N) return set_error(ALCM_E_INVALID, "ACT_T operand rows < N");
+  } else {
+    return set_error(ALCM_E_INVALID, "unknown B operand kind");
+  }
+  EpiDev& E = P.e;
+  E.bias = g.bias; E.acc_scale = g.acc_scale; E.out_scale = g.out_scale; E.act = g.act;
+  E.accumulate = g.accumulate; E.geglu = g.geglu; E.res = g.res;
+  E.r_sb = g.r_sb; E.r_st = g.r_st; E.r_sc = g.r_sc; E.r_zs1 = g.r_zs1; E.r_zs2 = g.r_zs2;
+  E.out = g.out; E.o_sb = g.o_sb; E.o_st = g.o_st; E.o_sc = g.o_sc; E.o_zs1 = g.o_zs1; E.o_zs2 = g.o_zs2;
+  E.orpb = FastDiv((uint32_t)(g.out_rows_per_batch > 0 ? g.out_rows_per_batch : 1));
+  E.out_step = g.out_step ? g.out_step : 1;
+  E.out_off = g.out_off;
+
+  const bool avec = act_vec_ok(g.a);
+  const bool split = g.split != 0;
+  const int N = g.N;
+  if (bkind == BK_W) {
+    if (N <= 32) {
+      if (avec) launch_split<256, 32, 4, 1, true, BK_W>(P, batch, N, split, s);
+      else launch_split<256, 32, 4, 1, false, BK_W>(P, batch, N, split, s);
+    } else if (N <= 64) {
+      if (avec) launch_split<256, 64, 4, 1, true, BK_W>(P, batch, N, split, s);
+      else launch_split<256, 64, 4, 1, false, BK_W>(P, batch, N, split, s);
+    } else {
+      if (avec) launch_split<128, 128, 2, 2, true, BK_W>(P, batch, N, split, s);
+      else launch_split<128, 128, 2, 2, false, BK_W>(P, batch, N, split, s);
+    }
+  } else {
+    if (!avec) return set_error(ALCM_E_INVALID, "attention GEMM A operand must be vectorisable");
+    if (bkind == BK_ACT) {
+      if (N <= 64) launch_split<256, 64, 4, 1, true, BK_ACT>(P, batch, N, split, s);
+      else launch_split<128, 128, 2, 2, true, BK_ACT>(P, batch, N, split, s);
+    } else {
+      if (N <= 64) launch_split<256, 64, 4, 1, true, BK_ACTT>(P, batch, N, split, s);
+      else launch_split<128, 128, 2, 2, true, BK_ACTT>(P, batch, N, split, s);
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(ALCM_E_HIP, std::string("gemm launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+// ---------------------------------------------------------------- weight packing (device)
+// W[co][ci][k] fp32 -> bf16 hi/lo [co][Kpad], K index = tap*cpad + ci.  For ConvTranspose1d
+// (weight [ci][co][k], stride s, phase r) tap j = r + s*(Q-1-tap).
+__global__ void pack_weight_kernel(const float* w, int c_out, int c_in, int ksz, int cpad, int kpad, int transposed,
+                                   int stride, int phase, u16* out) {
+  const int64_t total = (int64_t)c_out * kpad;
+  const int Q = transposed ? ksz / stride : ksz;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(idx / kpad);
+    const int k = (int)(idx % kpad);
+    const int tap = k / cpad, ci = k % cpad;
+    float v = 0.f;
+    if (tap < Q && ci < c_in) {
+      if (transposed) {
+        const int j = phase + stride * (Q - 1 - tap);
+        v = w[((int64_t)ci * c_out + co) * ksz + j];
+      } else {
+        v = w[((int64_t)co * c_in + ci) * ksz + tap];
+      }
+    }
+    const __bf16 h = (__bf16)v;
+    const __bf16 l = (__bf16)(v - (float)h);
+    out[idx] = __builtin_bit_cast(u16, h);
+    out[idx + total] = __builtin_bit_cast(u16, l);
+  }
+}
+
+int pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed, int stride,
+                     int phase, void* out, hipStream_t s) {
+  if (!w || !out || c_out <= 0 || c_in <= 0 || k <= 0 || cpad < c_in || cpad % 8 || kpad % BK)
+    return set_error(ALCM_E_INVALID, "pack_conv_weight: bad geometry");
+  const int Q = transposed ? k / stride : k;
+  if (transposed && (stride <= 0 || k % stride || phase < 0 || phase >= stride))
+    return set_error(ALCM_E_INVALID, "pack_conv_weight: bad transposed stride/phase");
+  if (Q * cpad > kpad) return set_error(ALCM_E_INVALID, "pack_conv_weight: kpad too small");
+  const int64_t total = (int64_t)c_out * kpad;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, w, c_out, c_in, k, cpad, kpad, transposed,
+                     stride, phase, (u16*)out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(ALCM_E_HIP, std::string("pack launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+}  // namespace alcm
+
+extern "C" int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream) {
+  if (!args) return alcm::set_error(ALCM_E_INVALID, "null args");
+  return alcm::gemm(*args, (hipStream_t)stream);
+}
+
+extern "C" int alcm_pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed,
+                                     int stride, int phase, void* out, alcm_stream_t stream) {
+  return alcm::pack_conv_weight(w, c_out, c_in, k, cpad, kpad, transposed, stride, phase, out, (hipStream_t)stream);
+}

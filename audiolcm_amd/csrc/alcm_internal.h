@@ -1,0 +1,46 @@
+// Internal (non-ABI) declarations shared by the libaudiolcm_hip.so translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "audiolcm_hip.h"
+
+namespace alcm {
+
+int set_error(int code, const std::string& msg);
+
+#define ALCM_HIP(expr)                                                                         \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return ::alcm::set_error(ALCM_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e));   \
+  } while (0)
+
+#define ALCM_TRY(expr)      \
+  do {                      \
+    int _r = (expr);        \
+    if (_r) return _r;      \
+  } while (0)
+
+int gemm(const alcm_gemm_args& g, hipStream_t s);
+int pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed, int stride,
+                     int phase, void* out, hipStream_t s);
+
+int group_norm_affine(const float* x, int B, int T, int C, int64_t sb, int64_t st, int groups, float eps,
+                      const float* gamma, const float* beta, float* scale, float* shift, hipStream_t s);
+int row_stats(const float* x, int rows, int C, int64_t ld, float eps, float* mean, float* rstd, hipStream_t s);
+int layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const float* gamma, const float* beta,
+               const float* add, int64_t ld_add, float* y, int64_t ld_out, hipStream_t s);
+int softmax_rows(float* x, int rows, int n, int64_t ld, hipStream_t s);
+int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st, const float* alpha_exp,
+                 const float* inv_beta, const float* up_filter, const float* down_filter, hipStream_t s);
+int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,
+             const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
+int fill_f32(float* p, int64_t n, float v, hipStream_t s);
+
+constexpr int kBK = 32;
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace alcm

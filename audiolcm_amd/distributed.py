@@ -1,0 +1,64 @@
+"""Multi-GPU prompt sharding: one process per GPU, RCCL all-gather of waveforms over xGMI.
+
+The path shards embarrassingly: prompts are independent and the
+per-prompt seeds make every clip independent of the shard it lands on.  Each rank
+generates a contiguous shard of the global batch; the only collective is one
+``all_gather_into_tensor`` of the decoded waveforms (backend "nccl" == RCCL on ROCm,
+"gloo" for the CPU tests).  Replaces the reference's rank-strided batch split
+(ldm/data/joinaudiodataset_anylen.py:165) used for its multi-GPU work.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous shard [lo, hi) of n items for `rank` (sizes differ by at most one)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
+    """torch.distributed init from RANK/WORLD_SIZE/LOCAL_RANK (torchrun); returns (rank, world, local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group(backend=backend or ("nccl" if torch.cuda.is_available() else "gloo"),
+                                rank=rank, world_size=world)
+    return rank, world, local
+
+
+def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
+    """Gather per-rank row blocks (contiguous shards of n_total rows) into the full (n_total, ...) tensor.
+
+    Shards are padded to the largest shard so a single all_gather_into_tensor moves everything."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return local
+    per = -(-n_total // world)
+    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    rows = [out[r * per: r * per + (shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0])]
+            for r in range(world)]
+    return torch.cat(rows, 0)
+
+
+def generate_sharded(generate_fn: Callable[[int, int], torch.Tensor], n_total: int, group=None) -> torch.Tensor:
+    """Run ``generate_fn(lo, hi) -> (hi-lo, N) waveforms`` on this rank's shard and all-gather the batch."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    lo, hi = shard_range(n_total, rank, world)
+    local = generate_fn(lo, hi)
+    return all_gather_rows(local, n_total, group)

@@ -1,0 +1,296 @@
+"""Thin torch-facing wrappers over the op-level C-ABI entry points.
+
+Each function takes CUDA (HIP) fp32 tensors, allocates its output with torch,
+and enqueues one or more libaudiolcm_hip kernels on the current stream.  They
+are the per-op drop-ins for the ATen ops the reference path runs
+(F.conv1d / conv_transpose1d / linear / group_norm / layer_norm / softmax,
+Activation1d, LCMSampler.step) and are what the op-level parity tests call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import _hip
+from ._hip import check, lib, ptr, stream_handle
+
+BK = 32
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class PackedWeight:
+    """bf16 hi/lo [rows][Kpad] GEMM operand (K index = tap*cpad + ci)."""
+    data: torch.Tensor  # uint16 (2, rows, kpad) on device
+    rows: int
+    cin: int
+    cpad: int
+    taps: int
+    kpad: int
+
+    @property
+    def lo_off(self) -> int:
+        return self.rows * self.kpad
+
+
+def pack_conv_weight(w: torch.Tensor, transposed: bool = False, stride: int = 1, phase: int = 0) -> PackedWeight:
+    """Pack Conv1d weight (Cout,Cin,K) — or ConvTranspose1d weight (Cin,Cout,K) for one phase."""
+    assert w.is_cuda and w.dtype == torch.float32
+    w = w.contiguous()
+    if w.dim() == 2:
+        w = w.unsqueeze(-1)
+    if transposed:
+        cin, cout, k = w.shape
+        taps = k // stride
+    else:
+        cout, cin, k = w.shape
+        taps = k
+    cpad = _round_up(cin, 8)
+    kpad = _round_up(taps * cpad, BK)
+    out = torch.empty((2, cout, kpad), dtype=torch.int16, device=w.device)
+    check(lib().alcm_pack_conv_weight(ptr(w), cout, cin, k, cpad, kpad, int(transposed), stride, phase, ptr(out),
+                                      stream_handle()), "pack_conv_weight")
+    return PackedWeight(out, cout, cin, cpad, taps, kpad)
+
+
+def _act_operand(x: torch.Tensor, sb: int, st: int, sc: int, T_in: int, C_in: int, cpad: int, ksize: int, dil: int,
+                 pad: int, up: int, rows_per_batch: int) -> _hip.Operand:
+    o = _hip.Operand()
+    o.kind = _hip.ALCM_OPND_ACT
+    o.ptr = ptr(x)
+    o.sb, o.st, o.sc = sb, st, sc
+    o.T_in, o.C_in, o.Cpad, o.ksize, o.dil, o.pad, o.up = T_in, C_in, cpad, ksize, dil, pad, up
+    o.rows_per_batch = rows_per_batch
+    return o
+
+
+def gemm(args: _hip.GemmArgs) -> None:
+    check(lib().alcm_gemm(C.byref(args), stream_handle()), "alcm_gemm")
+
+
+def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, padding: int = 0,
+           dilation: int = 1, upsample: int = 1, split: bool = True, channels_last: bool = False,
+           act: int = 0, residual: Optional[torch.Tensor] = None, packed: Optional[PackedWeight] = None,
+           prologue: Optional[dict] = None) -> torch.Tensor:
+    """F.conv1d(x, w, bias, padding=padding, dilation=dilation) on the MFMA implicit GEMM.
+
+    x is (B, Cin, T) (reference NCT layout) or, with channels_last, (B, T, Cin); the result
+    uses the same layout.  ``upsample=2`` applies nearest x2 to the input first
+    (F.interpolate(scale_factor=2, mode='nearest'))."""
+    pw = packed or pack_conv_weight(w)
+    if channels_last:
+        B, T, Cin = x.shape
+        sb, st, sc = x.stride()
+    else:
+        B, Cin, T = x.shape
+        sb, sc, st = x.stride()
+    K = pw.taps
+    Tu = T * upsample
+    Tout = Tu + 2 * padding - dilation * (K - 1)
+    assert Tout > 0
+    g = _hip.GemmArgs()
+    g.M, g.N, g.Kpad, g.batch, g.zdiv = B * Tout, pw.rows, pw.kpad, 1, 1
+    g.a = _act_operand(x, sb, st, sc, T, Cin, pw.cpad, K, dilation, padding, upsample, Tout)
+    if prologue:
+        g.a.pro_scale = ptr(prologue.get("scale"))
+        g.a.pro_shift = ptr(prologue.get("shift"))
+        g.a.pro_sb = prologue.get("sb", 0)
+        g.a.pro_mean = ptr(prologue.get("mean"))
+        g.a.pro_rstd = ptr(prologue.get("rstd"))
+        g.a.pro_act = prologue.get("act", 0)
+    b = _hip.Operand()
+    b.kind, b.ptr, b.rows, b.w_lo_off = _hip.ALCM_OPND_WEIGHT, ptr(pw.data), pw.rows, pw.lo_off
+    g.b = b
+    g.bias = ptr(bias)
+    g.acc_scale, g.out_scale, g.act = 1.0, 1.0, act
+    if channels_last:
+        out = torch.empty((B, Tout, pw.rows), device=x.device, dtype=torch.float32)
+        g.o_sb, g.o_st, g.o_sc = Tout * pw.rows, pw.rows, 1
+    else:
+        out = torch.empty((B, pw.rows, Tout), device=x.device, dtype=torch.float32)
+        g.o_sb, g.o_st, g.o_sc = pw.rows * Tout, 1, Tout
+    if residual is not None:
+        assert residual.shape == out.shape
+        r = residual
+        g.res = ptr(r)
+        if channels_last:
+            g.r_sb, g.r_st, g.r_sc = r.stride()
+        else:
+            g.r_sb, g.r_sc, g.r_st = r.stride()
+    g.out = ptr(out)
+    g.out_rows_per_batch, g.out_step, g.out_off = Tout, 1, 0
+    g.split = int(split)
+    gemm(g)
+    return out
+
+
+def conv_transpose1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
+                     split: bool = True) -> torch.Tensor:
+    """F.conv_transpose1d on NCT input as ``stride`` phase convolutions."""
+    B, Cin, T = x.shape
+    _, Cout, K = w.shape
+    assert K % stride == 0 and (K - stride) == 2 * padding, "polyphase form needs k = s*Q and pad = (k-s)/2"
+    Q = K // stride
+    Tout = T * stride
+    out = torch.empty((B, Cout, Tout), device=x.device, dtype=torch.float32)
+    sb, sc, st = x.stride()
+    for r in range(stride):
+        o = (r - padding) % stride
+        c = (o + padding - r) // stride
+        pw = pack_conv_weight(w, transposed=True, stride=stride, phase=r)
+        g = _hip.GemmArgs()
+        g.M, g.N, g.Kpad, g.batch, g.zdiv = B * T, Cout, pw.kpad, 1, 1
+        g.a = _act_operand(x, sb, st, sc, T, Cin, pw.cpad, Q, 1, Q - 1 - c, 1, T)
+        b = _hip.Operand()
+        b.kind, b.ptr, b.rows, b.w_lo_off = _hip.ALCM_OPND_WEIGHT, ptr(pw.data), pw.rows, pw.lo_off
+        g.b = b
+        g.bias = ptr(bias)
+        g.acc_scale, g.out_scale = 1.0, 1.0
+        g.out = ptr(out)
+        g.o_sb, g.o_st, g.o_sc = Cout * Tout, 1, Tout
+        g.out_rows_per_batch, g.out_step, g.out_off = T, stride, o
+        g.split = int(split)
+        gemm(g)
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, split: bool = True,
+           act: int = 0) -> torch.Tensor:
+    """F.linear on (..., K) rows."""
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1]).contiguous()
+    y = conv1d(x2.unsqueeze(0), w.unsqueeze(-1), bias, split=split, channels_last=True, act=act)
+    return y.reshape(*shp[:-1], w.shape[0])
+
+
+def bmm_nt(a: torch.Tensor, b: torch.Tensor, scale: float = 1.0, split: bool = True) -> torch.Tensor:
+    """(Z, M, K) x (Z, N, K)^T -> (Z, M, N): the Q K^T product of attention."""
+    Z, M, K = a.shape
+    N = b.shape[1]
+    assert K % 8 == 0 and a.is_contiguous() and b.is_contiguous()
+    out = torch.empty((Z, M, N), device=a.device, dtype=torch.float32)
+    g = _hip.GemmArgs()
+    g.M, g.N, g.Kpad, g.batch, g.zdiv = M, N, _round_up(K, BK), Z, 1
+    g.a = _act_operand(a, 0, K, 1, M, K, K, 1, 1, 0, 1, M)
+    g.a.zs1 = M * K
+    g.b = _act_operand(b, 0, K, 1, N, K, K, 1, 1, 0, 1, N)
+    g.b.zs1 = N * K
+    g.acc_scale, g.out_scale = scale, 1.0
+    g.out = ptr(out)
+    g.o_st, g.o_sc, g.o_zs1 = N, 1, M * N
+    g.out_rows_per_batch, g.out_step = M, 1
+    g.split = int(split)
+    gemm(g)
+    return out
+
+
+def bmm_nn(p: torch.Tensor, v: torch.Tensor, split: bool = True) -> torch.Tensor:
+    """(Z, M, K) x (Z, K, N) -> (Z, M, N): the P V product (V read N-contiguous)."""
+    Z, M, K = p.shape
+    N = v.shape[2]
+    Kp = _round_up(K, 8)
+    if Kp != K:
+        p = torch.nn.functional.pad(p, (0, Kp - K))
+    p = p.contiguous()
+    v = v.contiguous()
+    out = torch.empty((Z, M, N), device=p.device, dtype=torch.float32)
+    g = _hip.GemmArgs()
+    g.M, g.N, g.Kpad, g.batch, g.zdiv = M, N, _round_up(Kp, BK), Z, 1
+    g.a = _act_operand(p, 0, Kp, 1, M, Kp, Kp, 1, 1, 0, 1, M)
+    g.a.zs1 = M * Kp
+    b = _hip.Operand()
+    b.kind, b.ptr, b.st, b.sc, b.T_in, b.rows, b.zs1 = _hip.ALCM_OPND_ACT_T, ptr(v), N, 1, K, N, K * N
+    g.b = b
+    g.acc_scale, g.out_scale = 1.0, 1.0
+    g.out = ptr(out)
+    g.o_st, g.o_sc, g.o_zs1 = N, 1, M * N
+    g.out_rows_per_batch, g.out_step = M, 1
+    g.split = int(split)
+    gemm(g)
+    return out
+
+
+def group_norm_affine(x_cl: torch.Tensor, groups: int, gamma: torch.Tensor, beta: torch.Tensor,
+                      eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-(b, c) scale/shift equal to nn.GroupNorm on a channels-last (B, T, C) tensor."""
+    B, T, Cc = x_cl.shape
+    sb, st, sc = x_cl.stride()
+    assert sc == 1
+    scale = torch.empty((B, Cc), device=x_cl.device, dtype=torch.float32)
+    shift = torch.empty_like(scale)
+    check(lib().alcm_group_norm_affine(ptr(x_cl), B, T, Cc, sb, st, groups, eps, ptr(gamma), ptr(beta), ptr(scale),
+                                       ptr(shift), stream_handle()), "group_norm_affine")
+    return scale, shift
+
+
+def row_stats(x: torch.Tensor, eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    rows = x.numel() // x.shape[-1]
+    Cc = x.shape[-1]
+    x = x.contiguous()
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    check(lib().alcm_row_stats(ptr(x), rows, Cc, Cc, eps, ptr(mean), ptr(rstd), stream_handle()), "row_stats")
+    return mean, rstd
+
+
+def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    x = x.contiguous()
+    Cc = x.shape[-1]
+    rows = x.numel() // Cc
+    y = torch.empty_like(x)
+    check(lib().alcm_layer_norm(ptr(x), rows, Cc, Cc, eps, ptr(gamma), ptr(beta), None, 0, ptr(y), Cc,
+                                stream_handle()), "layer_norm")
+    return y
+
+
+def softmax_(x: torch.Tensor) -> torch.Tensor:
+    """In-place softmax over the last dim of a contiguous tensor."""
+    n = x.shape[-1]
+    rows = x.numel() // n
+    check(lib().alcm_softmax_rows(ptr(x), rows, n, n, stream_handle()), "softmax_rows")
+    return x
+
+
+def snake_params(alpha: torch.Tensor, beta: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """SnakeBeta logscale parameters -> (exp(alpha), 1/(exp(beta)+1e-9)) (activations.py:111-119)."""
+    return torch.exp(alpha), 1.0 / (torch.exp(beta) + 0.000000001)
+
+
+def activation1d(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor, up_filter: torch.Tensor,
+                 down_filter: torch.Tensor) -> torch.Tensor:
+    """Fused Activation1d(SnakeBeta) on a channels-last (B, T, C) tensor."""
+    B, T, Cc = x_cl.shape
+    x_cl = x_cl.contiguous()
+    ae, ib = snake_params(alpha, beta)
+    y = torch.empty_like(x_cl)
+    check(lib().alcm_activation1d(ptr(x_cl), ptr(y), B, T, Cc, T * Cc, Cc, ptr(ae.contiguous()),
+                                  ptr(ib.contiguous()), ptr(up_filter.reshape(-1).contiguous()),
+                                  ptr(down_filter.reshape(-1).contiguous()), stream_handle()), "activation1d")
+    return y
+
+
+def lcm_step(x: torch.Tensor, eps: torch.Tensor, noise: Optional[torch.Tensor], coeffs) -> Tuple[torch.Tensor,
+                                                                                                 torch.Tensor]:
+    """LCMSampler.step (eps prediction).  coeffs = (sqrt_a, sqrt_b, c_out, c_skip, sqrt_a_prev, sqrt_b_prev)."""
+    prev = torch.empty_like(x)
+    den = torch.empty_like(x)
+    arr = (C.c_float * 6)(*[float(c) for c in coeffs])
+    check(lib().alcm_lcm_step(ptr(x), ptr(eps), ptr(noise), arr, ptr(prev), ptr(den), x.numel(), stream_handle()),
+          "lcm_step")
+    return prev, den
+
+
+def sincos_embedding(v: torch.Tensor, freqs: torch.Tensor, scale: float, cos_first: bool) -> torch.Tensor:
+    B = v.shape[0]
+    half = freqs.numel()
+    out = torch.empty((B, 2 * half), device=v.device, dtype=torch.float32)
+    check(lib().alcm_sincos_embedding(ptr(v.float().contiguous()), scale, ptr(freqs), B, half, int(cos_first),
+                                      ptr(out), stream_handle()), "sincos_embedding")
+    return out

@@ -1,0 +1,183 @@
+/*
+ * audiolcm_hip.h — C-ABI of libaudiolcm_hip.so, the MI355X (gfx950) hot path of
+ * AudioLCM text-to-audio inference.
+ *
+ * Conventions:
+ *   - every entry point is `extern "C" int fn(...)`: 0 on success, a negative
+ *     ALCM_E* code otherwise; alcm_last_error() returns a thread-local message;
+ *   - every tensor argument is a caller-allocated DEVICE pointer (typically a
+ *     torch tensor's data_ptr()) in the reference's own layout unless stated,
+ *     fp32, contiguous; sizes are explicit;
+ *   - work is enqueued on the caller's hipStream_t (torch.cuda.current_stream());
+ *     no call allocates device memory except the *_create loaders, no call
+ *     synchronises the host, calls are re-entrant across streams;
+ *   - no torch types cross the boundary.
+ *
+ * Reference interfaces replaced (paths under the reference checkout):
+ *   alcm_dit_*          ConcatDiT2MLP.forward          ldm/modules/diffusionmodules/concatDiT.py:282-304
+ *                       (called as LCM_audio.apply_model, ldm/models/diffusion/lcm_audio.py:479-502)
+ *   alcm_lcm_step       LCMSampler.step (eps branch)   ldm/models/diffusion/scheduling_lcm.py:410-496
+ *   alcm_*_embedding    get_guidance_scale_embedding   scheduling_lcm.py:87-113
+ *                       TimestepEmbedder.timestep_embedding  concatDiT.py:49-67
+ *   alcm_vae_*          LCM_audio.decode_first_stage   lcm_audio.py:392-406 -> AutoencoderKL.decode
+ *                       autoencoder1d.py:59-62, Decoder1D.forward autoencoder1d.py:484-517
+ *   alcm_bigvgan_*      BigVGAN.forward                vocoder/bigvgan/models.py:181-203
+ *                       (VocoderBigVGAN.vocode, models.py:406-411)
+ *   alcm_activation1d   Activation1d.forward           vocoder/bigvgan/alias_free_torch/act.py:23-27
+ *   alcm_gemm           aten conv1d / conv_transpose1d / linear / bmm on the path (SURVEY.md §2 kernel inventory)
+ */
+#ifndef AUDIOLCM_HIP_H
+#define AUDIOLCM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* alcm_stream_t; /* hipStream_t */
+
+enum {
+  ALCM_OK = 0,
+  ALCM_E_INVALID = -1,  /* bad argument / shape */
+  ALCM_E_HIP = -2,      /* HIP runtime error */
+  ALCM_E_MISSING = -3,  /* required weight tensor missing */
+  ALCM_E_WORKSPACE = -4 /* workspace too small */
+};
+
+/* ---------------------------------------------------------------- misc */
+const char* alcm_last_error(void);
+int alcm_version(void);
+/* device properties check: returns 0 if device `dev` is gfx950 */
+int alcm_check_device(int dev);
+
+/* ---------------------------------------------------------------- generic MFMA GEMM / implicit-GEMM conv1d
+ * C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), bf16 MFMA (v_mfma_f32_16x16x32_bf16) with fp32
+ * accumulate; split=1 uses the 3-term bf16 split (hi*hi + hi*lo + lo*hi) for fp32-level accuracy. */
+enum { ALCM_OPND_ACT = 0, ALCM_OPND_ACT_T = 1, ALCM_OPND_WEIGHT = 2 };
+
+typedef struct alcm_operand {
+  int kind;
+  const void* ptr;
+  /* ACT: element (b, t, c) at ptr + b*sb + t*st + c*sc; K index k = tap*Cpad + ci, source time
+   *      t_src = t + tap*dil - pad (up == 2: nearest-x2 upsampled input, t_up = t + tap*dil - pad,
+   *      t_src = t_up/2), zero outside [0, T_in) / ci >= C_in / k >= ksize*Cpad.
+   * ACT_T: element (n, k) at ptr + k*st + n*sc, valid k < T_in, n < rows.
+   * WEIGHT: packed bf16 [rows][Kpad] hi plane at ptr, lo plane at ptr + w_lo_off (elements). */
+  int64_t sb, st, sc;
+  int T_in, C_in, Cpad, ksize, dil, pad, up;
+  int rows_per_batch; /* ACT: rows m -> (b = m / rows_per_batch, t = m % rows_per_batch) */
+  int rows;           /* ACT_T / WEIGHT: number of valid rows */
+  int64_t zs1, zs2;   /* batched offset (z / zdiv)*zs1 + (z % zdiv)*zs2 */
+  /* ACT prologue, applied to valid (non-padding) elements: v = (v - mean[b*T_in+t_src]) * rstd[...]
+   * (if pro_mean), v = v*pro_scale[b*pro_sb+c] + pro_shift[...] (if pro_scale), v = act(v) */
+  const float* pro_scale;
+  const float* pro_shift;
+  int64_t pro_sb;
+  const float* pro_mean;
+  const float* pro_rstd;
+  int pro_act;
+  int64_t w_lo_off;
+} alcm_operand;
+
+typedef struct alcm_gemm_args {
+  int M, N, Kpad; /* Kpad: multiple of 32 covering the real K */
+  int batch, zdiv;
+  alcm_operand a, b;
+  /* epilogue: v = acc*acc_scale + bias[n]; v = act(v) (geglu: v_even * gelu_erf(v_odd) -> column n/2);
+   *           v += res[...]; v *= out_scale; if accumulate v += out[...]; out[...] = v
+   * output row m -> (b, t), stored at out + zoff + b*o_sb + (t*out_step + out_off)*o_st + n*o_sc */
+  const float* bias;
+  float acc_scale, out_scale;
+  int act, accumulate, geglu;
+  const float* res;
+  int64_t r_sb, r_st, r_sc, r_zs1, r_zs2;
+  float* out;
+  int64_t o_sb, o_st, o_sc, o_zs1, o_zs2;
+  int out_rows_per_batch, out_step, out_off;
+  int split;
+} alcm_gemm_args;
+
+int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream);
+
+/* pack a conv/linear weight W[co][ci][k] (fp32, DEVICE) into the bf16 hi/lo [Cout][Kpad] layout with
+ * K index = tap*Cpad + ci. transposed=1 takes a ConvTranspose1d weight [ci][co][k] and a phase
+ * (stride s, phase r) selecting taps j = r + s*(Q-1-tap), Q = k/s. out must hold 2*Cout*Kpad u16. */
+int alcm_pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed,
+                          int stride, int phase, void* out, alcm_stream_t stream);
+
+/* ---------------------------------------------------------------- normalisation / elementwise
+ * Layout of x for the norm kernels: element (b, t, c) at x + b*sb + t*st + c (channels contiguous). */
+int alcm_group_norm_affine(const float* x, int B, int T, int C, int64_t sb, int64_t st, int groups,
+                           float eps, const float* gamma, const float* beta, float* scale_out,
+                           float* shift_out, alcm_stream_t stream);
+int alcm_row_stats(const float* x, int rows, int C, int64_t ld, float eps, float* mean, float* rstd,
+                   alcm_stream_t stream);
+int alcm_layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const float* gamma,
+                    const float* beta, const float* add, int64_t ld_add, float* y, int64_t ld_out,
+                    alcm_stream_t stream);
+int alcm_softmax_rows(float* x, int rows, int n, int64_t ld, alcm_stream_t stream);
+int alcm_activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st,
+                      const float* alpha_exp, const float* inv_beta, const float* up_filter,
+                      const float* down_filter, alcm_stream_t stream);
+
+/* ---------------------------------------------------------------- LCM scheduler pieces */
+/* coeffs (HOST array of 6): {sqrt_a, sqrt_b, c_out, c_skip, sqrt_a_prev, sqrt_b_prev};
+ * noise may be NULL (final step: prev_out = denoised) */
+int alcm_lcm_step(const float* x, const float* eps, const float* noise, const float* coeffs,
+                  float* prev_out, float* denoised_out, int64_t n, alcm_stream_t stream);
+/* classifier-free-guidance variant (config 4): eps = eps_uncond + cfg_scale*(eps_cond - eps_uncond)
+ * (plms.py:184-186 / ddim.py:203-205) fused into the same step */
+int alcm_lcm_step_cfg(const float* x, const float* eps_cond, const float* eps_uncond, float cfg_scale,
+                      const float* noise, const float* coeffs, float* prev_out, float* denoised_out, int64_t n,
+                      alcm_stream_t stream);
+/* out[b] = [f(v[b]*vscale*freqs[i]) ...]: cos_first ? [cos | sin] (TimestepEmbedder, concatDiT.py:49-67)
+ *                                                   : [sin | cos] (get_guidance_scale_embedding, w*1000).
+ * freqs: the reference's fp32 frequency table (half entries, device pointer) */
+int alcm_sincos_embedding(const float* v, float vscale, const float* freqs, int B, int half, int cos_first,
+                          float* out, alcm_stream_t stream);
+
+/* ---------------------------------------------------------------- models
+ * Weights are host fp32 tensors named by the reference state_dict keys. */
+typedef struct alcm_named_tensor {
+  const char* name;
+  const float* data; /* HOST pointer, contiguous fp32 */
+  int ndim;
+  int64_t shape[4];
+} alcm_named_tensor;
+
+typedef struct alcm_model alcm_model;
+
+/* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL decoder, 2 = BigVGAN.
+ * iconfig/fconfig: see DESIGN.md §C-ABI (hyper-parameters from configs/audiolcm.yaml / bigvgan json) */
+enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2 };
+int alcm_model_create(int kind, const int* iconfig, int n_iconfig, const alcm_named_tensor* tensors,
+                      int n_tensors, int split, alcm_model** out);
+int alcm_model_destroy(alcm_model* m);
+size_t alcm_model_weight_bytes(const alcm_model* m);
+int alcm_model_set_split(alcm_model* m, int split);
+
+/* DiT.  x (B,C_lat,T) NCT, t (B,) int64, ctx (B,154,1024), w_emb (B,256) -> eps (B,C_lat,T) NCT.
+ * cemb_cache: (B,154,hidden) device buffer filled by alcm_dit_embed_context (step-invariant, hoisted). */
+size_t alcm_dit_workspace_bytes(const alcm_model* m, int B, int T);
+int alcm_dit_embed_context(alcm_model* m, const float* ctx, int B, float* cemb_cache, void* ws,
+                           size_t ws_bytes, alcm_stream_t stream);
+int alcm_dit_forward(alcm_model* m, const float* x, const int64_t* t, const float* cemb_cache,
+                     const float* w_emb, float* eps_out, int B, int T, void* ws, size_t ws_bytes,
+                     alcm_stream_t stream);
+
+/* VAE decode_first_stage. z (B,20,T) NCT -> mel (B,80,2T) NCT */
+size_t alcm_vae_workspace_bytes(const alcm_model* m, int B, int T);
+int alcm_vae_decode(alcm_model* m, const float* z, float inv_scale_factor, float* mel_out, int B, int T,
+                    void* ws, size_t ws_bytes, alcm_stream_t stream);
+
+/* BigVGAN. mel (B,80,M) NCT -> wav (B,1,256*M) */
+size_t alcm_bigvgan_workspace_bytes(const alcm_model* m, int B, int M);
+int alcm_bigvgan_forward(alcm_model* m, const float* mel, float* wav_out, int B, int M, void* ws,
+                         size_t ws_bytes, alcm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AUDIOLCM_HIP_H */

@@ -1,0 +1,187 @@
+"""Op-level parity of the HIP kernels (through the C-ABI) against plain fp32 PyTorch on CPU.
+
+Tolerances: split (bf16x3) MFMA mode is fp32-accurate -> relative L2 <= 2e-5;
+plain bf16 MFMA mode -> relative L2 <= 1.5e-2.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+SPLIT_TOL = 2e-5
+BF16_TOL = 1.5e-2
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from audiolcm_amd import _hip, kernels
+    _hip.require_device(0)
+    return kernels
+
+
+def _r(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g) * scale
+
+
+def dev(t):
+    return t.cuda()
+
+
+@pytest.mark.parametrize("B,Cin,T,Cout,k,pad,dil,cl", [
+    (2, 24, 50, 40, 3, 1, 1, False),     # NCT (scalar loader), generic N tile
+    (2, 64, 37, 130, 9, 4, 1, True),     # vector loader, ragged M/N tiles, FFN-like k9
+    (1, 24, 300, 24, 11, 25, 5, True),   # BigVGAN tail: N=24 (256x32 tile), dilation 5
+    (3, 48, 129, 48, 7, 9, 3, True),     # N=48 (256x64 tile), dilation 3
+    (2, 20, 33, 576, 5, 2, 1, False),    # DiT proj_in: 20 channels (padded K)
+    (1, 24, 64, 1, 7, 3, 1, True),       # conv_post: N=1
+    (2, 80, 16, 1536, 7, 3, 1, False),   # conv_pre from NCT mel
+])
+@pytest.mark.parametrize("split", [True, False])
+def test_conv1d(K, B, Cin, T, Cout, k, pad, dil, cl, split):
+    x = _r((B, Cin, T), 1)
+    w = _r((Cout, Cin, k), 2, 1.0 / np.sqrt(Cin * k))
+    b = _r((Cout,), 3, 0.1)
+    ref = F.conv1d(x, w, b, padding=pad, dilation=dil)
+    xin = x.permute(0, 2, 1).contiguous() if cl else x
+    y = K.conv1d(dev(xin), dev(w), dev(b), padding=pad, dilation=dil, split=split, channels_last=cl).cpu()
+    if cl:
+        y = y.permute(0, 2, 1)
+    assert y.shape == ref.shape
+    assert rel_l2(y.numpy(), ref.numpy()) < (SPLIT_TOL if split else BF16_TOL)
+
+
+def test_conv1d_upsample_nearest(K):
+    x = _r((2, 768 // 8, 20), 4)
+    w = _r((64, 96, 3), 5, 0.1)
+    b = _r((64,), 6, 0.1)
+    ref = F.conv1d(F.interpolate(x, scale_factor=2.0, mode="nearest"), w, b, padding=1)
+    y = K.conv1d(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(b), padding=1, upsample=2,
+                 channels_last=True).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < SPLIT_TOL
+
+
+def test_conv1d_groupnorm_swish_prologue_and_residual(K):
+    B, T, Cc, Co = 2, 45, 64, 96
+    x = _r((B, Cc, T), 7, 2.0) + 0.5
+    gam, bet = 1 + _r((Cc,), 8, 0.1), _r((Cc,), 9, 0.1)
+    w, b = _r((Co, Cc, 3), 10, 0.08), _r((Co,), 11, 0.1)
+    res = _r((B, Co, T), 12)
+    h = F.group_norm(x, 32, gam, bet, 1e-6)
+    ref = F.conv1d(h * torch.sigmoid(h), w, b, padding=1) + res
+    xc = dev(x.permute(0, 2, 1).contiguous())
+    sc, sh = K.group_norm_affine(xc, 32, dev(gam), dev(bet), 1e-6)
+    y = K.conv1d(xc, dev(w), dev(b), padding=1, channels_last=True,
+                 residual=dev(res.permute(0, 2, 1).contiguous()),
+                 prologue=dict(scale=sc, shift=sh, sb=Cc, act=1)).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < SPLIT_TOL
+
+
+def test_conv1d_layernorm_prologue(K):
+    B, T, Cc = 2, 31, 64
+    x = _r((B, T, Cc), 13, 3.0) + 1.0
+    gam, bet = 1 + _r((Cc,), 14, 0.1), _r((Cc,), 15, 0.1)
+    w, b = _r((128, Cc, 9), 16, 0.05), _r((128,), 17, 0.1)
+    ln = F.layer_norm(x, (Cc,), gam, bet, 1e-5)
+    ref = F.conv1d(ln.permute(0, 2, 1), w, b, padding=4)
+    xd = dev(x)
+    mean, rstd = K.row_stats(xd, 1e-5)
+    y = K.conv1d(xd, dev(w), dev(b), padding=4, channels_last=True,
+                 prologue=dict(scale=dev(gam), shift=dev(bet), sb=0, mean=mean, rstd=rstd)).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < SPLIT_TOL
+
+
+@pytest.mark.parametrize("Cin,Cout,k,s", [(64, 32, 8, 4), (48, 24, 4, 2), (1536 // 16, 768 // 16, 8, 4)])
+def test_conv_transpose1d(K, Cin, Cout, k, s):
+    x = _r((2, Cin, 19), 18)
+    w = _r((Cin, Cout, k), 19, 1.0 / np.sqrt(Cin * k / s))
+    b = _r((Cout,), 20, 0.1)
+    ref = F.conv_transpose1d(x, w, b, stride=s, padding=(k - s) // 2)
+    y = K.conv_transpose1d(dev(x), dev(w), dev(b), s, (k - s) // 2).cpu()
+    assert y.shape == ref.shape
+    assert rel_l2(y.numpy(), ref.numpy()) < SPLIT_TOL
+
+
+@pytest.mark.parametrize("Z,L,d", [(4, 467, 72), (2, 40, 1536)])
+def test_attention_products(K, Z, L, d):
+    q, k, v = _r((Z, L, d), 21), _r((Z, L, d), 22), _r((Z, L, d), 23)
+    sim = torch.einsum("bid,bjd->bij", q, k) * d ** -0.5
+    s = K.bmm_nt(dev(q), dev(k), d ** -0.5).cpu()
+    assert rel_l2(s.numpy(), sim.numpy()) < SPLIT_TOL
+    p = sim.softmax(-1)
+    pd = K.softmax_(dev(sim.clone())).cpu()
+    np.testing.assert_allclose(pd.numpy(), p.numpy(), rtol=1e-5, atol=1e-7)
+    o = K.bmm_nn(dev(p), dev(v)).cpu()
+    assert rel_l2(o.numpy(), torch.einsum("bij,bjd->bid", p, v).numpy()) < SPLIT_TOL
+
+
+def test_linear_and_layer_norm(K):
+    x = _r((3, 77, 1024), 24)
+    w, b = _r((576, 1024), 25, 1 / 32.0), _r((576,), 26, 0.1)
+    y = K.linear(dev(x), dev(w), dev(b), act=3).cpu()
+    assert rel_l2(y.numpy(), F.gelu(F.linear(x, w, b), approximate="tanh").numpy()) < SPLIT_TOL
+    g, be = 1 + _r((576,), 27, 0.1), _r((576,), 28, 0.1)
+    ln = K.layer_norm(dev(y), dev(g), dev(be), 1e-5).cpu()
+    ref = F.layer_norm(F.gelu(F.linear(x, w, b), approximate="tanh"), (576,), g, be, 1e-5)
+    assert rel_l2(ln.numpy(), ref.numpy()) < SPLIT_TOL
+
+
+def test_group_norm_stats(K):
+    x = _r((2, 36, 467), 29, 3.0) + 2.0
+    g, b = 1 + _r((36,), 30, 0.1), _r((36,), 31, 0.1)
+    ref = F.group_norm(x, 6, g, b, 1e-6)
+    sc, sh = K.group_norm_affine(dev(x.permute(0, 2, 1).contiguous()), 6, dev(g), dev(b), 1e-6)
+    y = x * sc.cpu()[:, :, None] + sh.cpu()[:, :, None]
+    assert rel_l2(y.numpy(), ref.numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["act1d_T50.npz", "act1d_T3.npz"])
+def test_activation1d_golden(K, name):
+    g = golden(name)
+    x = torch.from_numpy(g["x"])
+    y = K.activation1d(dev(x.permute(0, 2, 1).contiguous()), *(dev(torch.from_numpy(g[k])) for k in
+                       ("alpha", "beta", "up_filter", "down_filter"))).cpu().permute(0, 2, 1)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=2e-5, atol=2e-6)
+
+
+def test_activation1d_long(K):
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    C, T = 96, 1000
+    x = _r((2, C, T), 32, 1.5)
+    a, b = _r((C,), 33, 0.3), _r((C,), 34, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    ref = O.activation1d(x, a, b, f, f)
+    y = K.activation1d(dev(x.permute(0, 2, 1).contiguous()), dev(a), dev(b), dev(f), dev(f)).cpu().permute(0, 2, 1)
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=2e-5, atol=5e-6)
+
+
+def test_lcm_step_golden(K):
+    from oracle import alcm_oracle as O
+    g = golden("lcm_step.npz")
+    ac = O.alphas_cumprod()
+    x, eps, nz = (dev(torch.from_numpy(g[k])) for k in ("x", "eps", "noise"))
+    for t, pt, xin, noise, kp, kd in ((999, 499, x, nz, "prev0", "den0"), (499, 499, None, None, "prev1", "den1")):
+        sc = O.lcm_step_scalars(t, pt, ac)
+        coeffs = [sc[k].item() for k in ("sqrt_a", "sqrt_b", "c_out", "c_skip", "sqrt_a_prev", "sqrt_b_prev")]
+        xx = xin if xin is not None else dev(torch.from_numpy(g["prev0"]))
+        prev, den = K.lcm_step(xx, eps, noise, coeffs)
+        np.testing.assert_allclose(prev.cpu().numpy(), g[kp], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(den.cpu().numpy(), g[kd], rtol=1e-6, atol=1e-6)
+
+
+def test_embeddings_golden(K):
+    from audiolcm_amd import schedule
+    g = golden("schedule.npz")
+    t = torch.from_numpy(g["t"])
+    te = K.sincos_embedding(dev(t.float()), dev(schedule.timestep_freqs()), 1.0, True).cpu()
+    np.testing.assert_allclose(te.numpy(), g["timestep_emb"], atol=2e-6)
+    w = torch.full((3,), 4.0)
+    ge = K.sincos_embedding(dev(w), dev(schedule.guidance_freqs()), 1000.0, False).cpu()
+    np.testing.assert_allclose(ge.numpy(), g["guidance_w4"], atol=2e-6)
