@@ -44,6 +44,11 @@ class NamedTensor(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data", vp), ("ndim", C.c_int), ("shape", i64 * 4)]
 
 
+class ProfEntry(C.Structure):
+    _fields_ = [("name", C.c_char * 128), ("launches", i64), ("total_ms", C.c_double), ("flops", C.c_double),
+                ("bytes", C.c_double), ("roof_ms", C.c_double)]
+
+
 # (name, restype, argtypes) — every symbol include/audiolcm_hip.h declares
 _SIGS = [
     ("alcm_last_error", C.c_char_p, []),
@@ -73,6 +78,8 @@ _SIGS = [
     ("alcm_vae_decode", C.c_int, [vp, fp, C.c_float, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
     ("alcm_bigvgan_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_bigvgan_forward", C.c_int, [vp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+    ("alcm_profile_begin", C.c_int, [C.c_double, C.c_double]),
+    ("alcm_profile_end", C.c_int, [C.POINTER(ProfEntry), C.c_int, C.POINTER(C.c_int)]),
 ]
 EXPORTED = [s[0] for s in _SIGS]
 
@@ -126,3 +133,21 @@ def ptr(t) -> Optional[int]:
     if t is None:
         return None
     return int(t.data_ptr())
+
+
+PEAK_BF16_FLOPS = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
+PEAK_HBM_BYTES = 8.0e12    # MI355X HBM3E (spec)
+
+
+def profile_begin(peak_flops: float = PEAK_BF16_FLOPS, peak_bytes: float = PEAK_HBM_BYTES) -> None:
+    check(lib().alcm_profile_begin(peak_flops, peak_bytes), "alcm_profile_begin")
+
+
+def profile_end(max_entries: int = 256):
+    """-> list of dicts {name, launches, total_ms, flops, bytes} (synchronises the recorded events)."""
+    arr = (ProfEntry * max_entries)()
+    n = C.c_int(0)
+    check(lib().alcm_profile_end(arr, max_entries, C.byref(n)), "alcm_profile_end")
+    return [dict(name=arr[i].name.decode(), launches=int(arr[i].launches), total_ms=float(arr[i].total_ms),
+                 flops=float(arr[i].flops), bytes=float(arr[i].bytes), roof_ms=float(arr[i].roof_ms))
+            for i in range(min(n.value, max_entries))]

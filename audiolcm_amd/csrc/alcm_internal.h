@@ -40,6 +40,10 @@ int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, co
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
 
+bool prof_enabled();
+void* prof_start(hipStream_t s);
+void prof_stop(void* tok, hipStream_t s, const std::string& name, double flops, double bytes);
+
 constexpr int kBK = 32;
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

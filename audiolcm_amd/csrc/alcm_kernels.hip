@@ -251,8 +251,12 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
   const int runs = (T + A1D_R - 1) / A1D_R;
   const int64_t total = (int64_t)B * runs * C;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+  void* tok = prof_start(s);
   hipLaunchKernelGGL(act1d_kernel, dim3(blocks), dim3(256), 0, s, x, y, B, T, C, sb, st, alpha_exp, inv_beta,
                      up_filter, down_filter, runs, total);
+  // per output sample: 12 up-FIR + 12 down-FIR MACs on 2 upsampled samples, 2 sin; 4 B in + 4 B out
+  prof_stop(tok, s, "alcm::act1d_kernel(float const*, float*, int, int, int, long, long, float const*, float const*, "
+            "float const*, float const*, int, long)", 2.0 * 36.0 * B * (double)T * C, 8.0 * B * (double)T * C);
   ALCM_HIP(hipGetLastError());
   return 0;
 }

@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""bench.py — AudioLCM text-to-audio hot path on MI355X: generated audio-seconds per second.
+
+One "step" = one pass of the hot path over one batch of synthetic prompts: LCM sampler
+(S DiT calls + fused LCM steps) -> VAE decode_first_stage -> BigVGAN vocoder, with the
+conditioning embeddings and per-prompt seeds already resident in HBM (text encoders are
+out of scope); for N>1 each rank runs its own shard of 32 prompts and the
+waveforms are all-gathered over RCCL (weak scaling, BASELINE config 3).
+
+Workload at N=1: BASELINE.json configs[1] — batch 32 AudioCaps-shaped prompts, 2 LCM steps,
+10 s clips (latent 20x312, mel 80x624, 159,744 samples @16 kHz).  Weights are the seeded
+synthetic recipe (no checkpoints offline).
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline fields.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "generated audio-sec/s (real-time factor), 2-step LCM batch=32, 1/2/4/8 GPU"
+SR, HOP = 16000, 256
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32, help="prompts per GPU")
+    ap.add_argument("--lcm-steps", type=int, default=2)
+    ap.add_argument("--latent-len", type=int, default=312)
+    ap.add_argument("--mode", choices=["split", "bf16"], default="split",
+                    help="split: bf16x3 MFMA (fp32-parity); bf16: single bf16 MFMA")
+    ap.add_argument("--also-other-mode", type=int, default=1, help="N=1: also time the other precision mode")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-clips", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(clips: int, latent_len: int, lcm_steps: int):
+    """The oracle (fp32 PyTorch-CPU restatement of the reference path) on a bounded sample."""
+    from audiolcm_amd import recipe
+    from oracle import alcm_oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    Wd, Wv, Wg = recipe.dit_state(0), recipe.vae_state(0), recipe.bigvgan_state(0)
+    ctx = recipe.synthetic_context(clips)
+    xT, noise = recipe.prompt_noise(range(clips), lcm_steps, 20, latent_len)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for i in range(clips):  # per clip, as the reference API (InferAPI.py:159-163)
+            O.generate(Wd, Wv, Wg, ctx[i:i + 1], xT[i:i + 1], noise[:, i:i + 1], S=lcm_steps)
+    dt = time.perf_counter() - t0
+    audio = clips * latent_len * 2 * HOP / SR
+    return dict(value=round(audio / dt, 4), unit="audio-s/s", cores=threads, kind="port",
+                sample=f"{clips} clip(s) x {lcm_steps} LCM steps, {audio / clips:.3f} s each, batch 1 per clip, "
+                       f"fp32 torch-CPU oracle, {dt:.1f} s wall")
+
+
+def main():
+    a = parse()
+    from audiolcm_amd import _hip, recipe
+    from audiolcm_amd.distributed import all_gather_rows, init_from_env
+    from audiolcm_amd.pipeline import AudioLCMPipeline
+    import torch.distributed as dist
+
+    rank, world, local = init_from_env()
+    torch.cuda.set_device(local)
+    _hip.require_device(local)
+    B, S, T = a.batch, a.lcm_steps, a.latent_len
+    pipe = AudioLCMPipeline.from_recipe(0, split=(a.mode == "split"))
+    ids = list(range(rank * B, (rank + 1) * B))
+    cond = torch.cat([recipe.synthetic_context(1, seed0=1000 + i) for i in ids], 0).cuda()
+    clip_sec = T * 2 * HOP / SR
+
+    def step():
+        out = pipe.generate(cond, seeds=ids, steps=S, latent_len=T)
+        if world > 1:
+            all_gather_rows(out["wav"], B * world)
+        return out
+
+    def timed(k, profile):
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if profile:
+            _hip.profile_begin()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        prof = _hip.profile_end() if profile else []
+        if world > 1:
+            t = torch.tensor([dt], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, prof
+
+    dt, prof = timed(a.steps, True)
+    value = world * B * clip_sec * a.steps / dt
+    gpu_ms = sum(p["total_ms"] for p in prof)
+    dom = max(prof, key=lambda p: p["total_ms"]) if prof else None
+    roofline = None
+    if dom:
+        mfma = dom["flops"] / max(dom["bytes"], 1) > _hip.PEAK_BF16_FLOPS / _hip.PEAK_HBM_BYTES
+        sec = dom["total_ms"] / 1e3
+        if mfma:
+            ach, peak, unit = dom["flops"] / sec / 1e12, _hip.PEAK_BF16_FLOPS / 1e12, "TFLOP/s"
+        else:
+            ach, peak, unit = dom["bytes"] / sec / 1e9, _hip.PEAK_HBM_BYTES / 1e9, "GB/s"
+        roofline = dict(bound="mfma" if mfma else "hbm", achieved=round(ach, 2), peak=peak, unit=unit,
+                        frac=round(ach / peak, 4), traffic=None, kernel=dom["name"], launches=dom["launches"],
+                        avg_launch_us=round(1e3 * dom["total_ms"] / dom["launches"], 2),
+                        per_launch_algorithmic=round((dom["flops"] if mfma else dom["bytes"]) / dom["launches"], 1),
+                        kernel_share_of_gpu_time=round(dom["total_ms"] / max(gpu_ms, 1e-9), 4),
+                        path_roofline_frac=round(sum(p["roof_ms"] for p in prof) / (1e3 * dt), 4),
+                        path_roofline_note="sum over all kernel launches of max(F/2.5PF, B/8TB/s) / measured wall")
+    line = dict(metric=METRIC, value=round(value, 2), unit="audio-s/s", n_gpus=world, steps=a.steps,
+                warmup=a.warmup, ms_per_step=round(1e3 * dt / a.steps, 2), higher_is_better=True, scaling="weak",
+                vs_baseline=None,
+                dtype="bf16x3-split MFMA (fp32 accumulate, fp32 activations)" if a.mode == "split"
+                else "bf16 MFMA (fp32 accumulate, fp32 activations)",
+                data="synthetic (seeded recipe weights, N(0,1) conditioning, per-prompt seeds)",
+                config=dict(workload=f"BASELINE configs[1]: batch={B} prompts/GPU, {S} LCM steps, "
+                                     f"{clip_sec:.3f} s clips (latent 20x{T}, mel 80x{2 * T}, {2 * T * HOP} samples)",
+                            global_batch=B * world, per_gpu_batch=B, lcm_steps=S, latent_len=T,
+                            parallelism=f"dp{world} (prompt shards, RCCL all-gather of waveforms)"),
+                roofline=roofline)
+    if world == 1 and a.also_other_mode:
+        other = "bf16" if a.mode == "split" else "split"
+        pipe.set_split(other == "split")
+        dt2, _ = timed(a.steps, False)
+        pipe.set_split(a.mode == "split")
+        line[f"{other}_mode"] = dict(value=round(B * clip_sec * a.steps / dt2, 2),
+                                     ms_per_step=round(1e3 * dt2 / a.steps, 2))
+    if rank == 0 and world == 1 and a.cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(a.cpu_clips, T, S)
+    if rank == 0:
+        line["kernels"] = sorted(({k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.items()}
+                                  for p in prof), key=lambda p: -p["total_ms"])[:8]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

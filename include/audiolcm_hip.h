@@ -177,6 +177,21 @@ size_t alcm_bigvgan_workspace_bytes(const alcm_model* m, int B, int M);
 int alcm_bigvgan_forward(alcm_model* m, const float* mel, float* wav_out, int B, int M, void* ws,
                          size_t ws_bytes, alcm_stream_t stream);
 
+/* ---------------------------------------------------------------- live kernel timing (bench.py roofline)
+ * Between begin/end every kernel launch is bracketed by hipEvents on its stream; end synchronises
+ * and returns per-kernel aggregates keyed by the demangled kernel name rocprofv3 reports.
+ * flops/bytes are ALGORITHMIC (2*M*N*K for GEMMs; unique input + weight + output bytes). */
+typedef struct alcm_prof_entry {
+  char name[128];
+  int64_t launches;
+  double total_ms;
+  double flops;
+  double bytes;
+  double roof_ms; /* sum over launches of max(flops/peak_flops, bytes/peak_bw) */
+} alcm_prof_entry;
+int alcm_profile_begin(double peak_flops, double peak_bytes_per_s);
+int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_entries);
+
 #ifdef __cplusplus
 }
 #endif

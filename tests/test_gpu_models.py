@@ -155,3 +155,18 @@ def test_latent_length_limit(M):
     x = torch.zeros((1, 20, 846), device="cuda")
     with pytest.raises(ValueError):
         M["dit"](x, torch.zeros(1, dtype=torch.long, device="cuda"), torch.zeros((1, 154, 1024), device="cuda"))
+
+
+def test_batch_infer_api_writes_wavs(tmp_path):
+    """AudioLCMBatchInfer end to end on the YAML surface (synthetic weights): PCM16 WAV per prompt."""
+    import os
+    from audiolcm_amd.infer_api import AudioLCMBatchInfer
+    from audiolcm_amd.wavio import read_pcm16
+    from conftest import REPO
+    prompts = ["a dog barks", "rain falls on a tin roof", "a car passes by"]
+    path = AudioLCMBatchInfer(prompts, config_path=os.path.join(REPO, "configs", "audiolcm.yaml"),
+                              synthetic_seed=0, batch_size=2, outpath=str(tmp_path))
+    assert path == os.path.join(str(tmp_path), "a-car-passes-by_0.wav")
+    for p in prompts:
+        data, sr = read_pcm16(os.path.join(str(tmp_path), p.replace(" ", "-") + "_0.wav"))
+        assert sr == 16000 and data.shape == (159744,) and np.abs(data).max() > 0

@@ -168,3 +168,25 @@ def test_product_fails_loudly_without_library(monkeypatch):
     monkeypatch.setattr(_hip, "_lib", None)
     with pytest.raises(ImportError):
         _hip.lib()
+
+
+def test_yaml_instantiates_lcm_model_without_gpu():
+    from audiolcm_amd import config, lcm, models, conditioning
+    cfg = config.load_config(os.path.join(REPO, "configs", "audiolcm.yaml"))
+    m = config.instantiate_from_config(cfg.model, split=True)
+    assert isinstance(m, lcm.LCM_audio)
+    assert isinstance(m.unet.diffusion_model, models.ConcatDiT2MLP)
+    assert m.unet.diffusion_model.cfg.hidden_size == 576 and m.unet.diffusion_model.cfg.depth == 4
+    assert isinstance(m.first_stage_model, models.AutoencoderKL)
+    assert m.first_stage_model.cfg.upsample_levels == (1,)
+    assert isinstance(m.cond_stage_model, conditioning.FrozenCLAPFLANEmbedder)
+    assert not m.unet.diffusion_model.loaded
+    with pytest.raises(RuntimeError):
+        m.unet.diffusion_model.forward_cached(torch.zeros(1, 20, 8), torch.zeros(1), None, None)
+
+
+def test_api_requires_checkpoints(tmp_path):
+    from audiolcm_amd.infer_api import AudioLCMBatchInfer
+    with pytest.raises(FileNotFoundError):
+        AudioLCMBatchInfer(["x"], config_path=os.path.join(REPO, "configs", "audiolcm.yaml"),
+                           model_path=str(tmp_path / "missing.ckpt"), outpath=str(tmp_path))
