@@ -37,7 +37,16 @@ class GemmArgs(C.Structure):
                 ("act", C.c_int), ("accumulate", C.c_int), ("geglu", C.c_int), ("res", fp),
                 ("r_sb", i64), ("r_st", i64), ("r_sc", i64), ("r_zs1", i64), ("r_zs2", i64), ("out", fp),
                 ("o_sb", i64), ("o_st", i64), ("o_sc", i64), ("o_zs1", i64), ("o_zs2", i64),
-                ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("split", C.c_int)]
+                ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("split", C.c_int),
+                ("disable_window", C.c_int)]
+
+
+class AmpArgs(C.Structure):
+    _fields_ = [("x", fp), ("B", C.c_int), ("T", C.c_int), ("Cin", C.c_int), ("act", C.c_int),
+                ("alpha_exp", fp), ("inv_beta", fp), ("up_filter", fp), ("down_filter", fp), ("w", vp),
+                ("w_lo_off", i64), ("kpad", C.c_int), ("Cout", C.c_int), ("ksize", C.c_int), ("dil", C.c_int),
+                ("pad", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
+                ("accumulate", C.c_int), ("out_scale", C.c_float), ("split", C.c_int)]
 
 
 class NamedTensor(C.Structure):
@@ -63,6 +72,7 @@ _SIGS = [
     ("alcm_layer_norm", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, fp, i64, fp, i64, vp]),
     ("alcm_softmax_rows", C.c_int, [fp, C.c_int, C.c_int, i64, vp]),
     ("alcm_activation1d", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, i64, i64, fp, fp, fp, fp, vp]),
+    ("alcm_amp_conv", C.c_int, [C.POINTER(AmpArgs), vp]),
     ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_lcm_step_cfg", C.c_int, [fp, fp, fp, C.c_float, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_sincos_embedding", C.c_int, [fp, C.c_float, fp, C.c_int, C.c_int, C.c_int, fp, vp]),

@@ -369,6 +369,191 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
   }
 }
 
+// ---------------------------------------------------------------- window convolution (ksize > 1)
+// Implicit GEMM for conv1d with k taps where the A operand of every tap is a shifted view of
+// one input window: for each 32-channel chunk the rows [t0 - pad, t0 + BM + (k-1)*dil - pad)
+// are loaded, normalised/activated (prologue) and split to bf16 hi/lo ONCE into LDS, and the k
+// taps then read it at row offset tap*dil.  Compared with the tap-by-tap loader this cuts the A
+// global loads, the fp32->bf16 conversions and the A LDS writes by k (k = 3..11 on the path).
+// Tiles never straddle a batch (grid.x = B * ceil(T_out / BM)); K order = (chunk, tap).
+constexpr int HALO_MAX = 64;
+
+template <int BM, int BN, int WM, int WN, bool SPLIT>
+__global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_per_batch, int T_out) {
+  constexpr int TM = BM / (WM * 16);
+  constexpr int TN = BN / (WN * 16);
+  constexpr int NP = SPLIT ? 2 : 1;
+  constexpr int WR_MAX = BM + HALO_MAX;
+  constexpr int WCH = WR_MAX * 4;
+  constexpr int WPER = (WCH + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) __bf16 Aw[NP][WR_MAX * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][NP][BN * LDS_ROW];
+
+  const ActDev& A = P.a;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int b = blockIdx.x / tiles_per_batch;
+  const int t0 = (blockIdx.x - b * tiles_per_batch) * BM;
+  const int col0 = blockIdx.y * BN;
+  const int WR = BM + (A.ksize - 1) * A.dil;
+  const float* xb = A.p + (int64_t)b * A.sb;
+  const int nC = A.Cpad / 32;
+  const int steps = nC * A.ksize;
+
+  float wv[WPER][8];
+  auto load_window = [&](int cc) {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = tid + i * 256;
+      const int w = c >> 2, kc = c & 3;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wv[i][j] = 0.f;
+      if (c >= WCH || w >= WR) continue;
+      const int tu = t0 + w - A.pad;
+      int ts = tu;
+      if (A.up == 2) {
+        if (tu < 0 || tu >= 2 * A.T_in) continue;
+        ts = tu >> 1;
+      } else if (tu < 0 || tu >= A.T_in) {
+        continue;
+      }
+      const int ci = cc * 32 + kc * 8;
+      const float* src = xb + (int64_t)ts * A.st + ci;
+      const float4 x0 = *reinterpret_cast<const float4*>(src);
+      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+      wv[i][0] = x0.x; wv[i][1] = x0.y; wv[i][2] = x0.z; wv[i][3] = x0.w;
+      wv[i][4] = x1.x; wv[i][5] = x1.y; wv[i][6] = x1.z; wv[i][7] = x1.w;
+      if (A.pm) {
+        const int64_t ri = (int64_t)b * A.T_in + ts;
+        const float mu = A.pm[ri], rs = A.pr[ri];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wv[i][j] = (wv[i][j] - mu) * rs;
+      }
+      if (A.ps) {
+        const float* sc = A.ps + (int64_t)b * A.psb + ci;
+        const float* sh = A.ph + (int64_t)b * A.psb + ci;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wv[i][j] = wv[i][j] * sc[j] + sh[j];
+      }
+      if (A.pact) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wv[i][j] = alcm_act(wv[i][j], A.pact);
+      }
+    }
+  };
+  auto store_window = [&]() {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = tid + i * 256;
+      const int w = c >> 2, kc = c & 3;
+      if (c >= WCH || w >= WR) continue;
+      split_store(wv[i], Aw[0] + w * LDS_ROW + kc * 8, Aw[NP - 1] + w * LDS_ROW + kc * 8, SPLIT);
+    }
+  };
+
+  WTile<BN> bt;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_window(0);
+  bt.load(P.w, tid, col0, 0, SPLIT);
+  store_window();
+  bt.template store<SPLIT>(Bs[0][0], Bs[0][NP - 1], tid);
+  __syncthreads();
+
+  const int a_base = (wm * TM * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
+  const int b_off = (wn * TN * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
+  int cc = 0, tap = 0;
+  for (int s = 0; s < steps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < steps;
+    if (more) {
+      const int ntap = tap + 1 == A.ksize ? 0 : tap + 1;
+      const int ncc = tap + 1 == A.ksize ? cc + 1 : cc;
+      bt.load(P.w, tid, col0, ntap * A.Cpad + ncc * 32, SPLIT);
+    }
+    const bool new_window = (tap == A.ksize - 1) && (cc + 1 < nC);
+    if (tap == 0 && cc + 1 < nC) load_window(cc + 1);
+
+    const int a_off = a_base + tap * A.dil * LDS_ROW;
+    bf16x8 ah[TM], bh[TN];
+    bf16x8 al[SPLIT ? TM : 1], bl[SPLIT ? TN : 1];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(&Aw[0][a_off + i * 16 * LDS_ROW]);
+      if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(&Aw[NP - 1][a_off + i * 16 * LDS_ROW]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][0][b_off + j * 16 * LDS_ROW]);
+      if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][NP - 1][b_off + j * 16 * LDS_ROW]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (SPLIT) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+
+    if (more) bt.template store<SPLIT>(Bs[cur ^ 1][0], Bs[cur ^ 1][NP - 1], tid);
+    if (new_window) {
+      __syncthreads();
+      store_window();
+    }
+    __syncthreads();
+    if (++tap == A.ksize) {
+      tap = 0;
+      ++cc;
+    }
+  }
+
+  // epilogue (rows are (b, t0 + local) directly)
+  const EpiDev& E = P.e;
+#pragma clang loop unroll(full)
+  for (int i = 0; i < TM; ++i) {
+#pragma clang loop unroll(full)
+    for (int r = 0; r < 4; ++r) {
+      const int tt = t0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+      const bool mok = tt < T_out;
+      const int64_t to = (int64_t)tt * E.out_step + E.out_off;
+      const int64_t obase = (int64_t)b * E.o_sb + to * E.o_st;
+      const int64_t rbase = (int64_t)b * E.r_sb + to * E.r_st;
+#pragma clang loop unroll(full)
+      for (int j = 0; j < TN; ++j) {
+        const int n = col0 + wn * TN * 16 + j * 16 + (lane & 15);
+        float v = acc[i][j][r] * E.acc_scale;
+        if (E.bias && n < P.N) v += E.bias[n];
+        int nout = n;
+        bool st = mok && n < P.N;
+        if (E.geglu) {
+          const float g = __shfl_xor(v, 1);
+          v = v * alcm_act(g, ACT_GELU_ERF);
+          st = st && ((lane & 1) == 0);
+          nout = n >> 1;
+        } else if (E.act) {
+          v = alcm_act(v, E.act);
+        }
+        if (st) {
+          if (E.res) v += E.res[rbase + (int64_t)nout * E.r_sc];
+          v *= E.out_scale;
+          float* o = E.out + obase + (int64_t)nout * E.o_sc;
+          if (E.accumulate) v += *o;
+          *o = v;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host side
 static bool fill_act(const alcm_operand& o, int M, ActDev& d, std::string& err) {
   d.p = (const float*)o.ptr;
@@ -423,6 +608,20 @@ template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND>
 static void launch_split(const GemmDev& P, int batch, int ncols, bool split, hipStream_t s) {
   if (split) launch_one<BM, BN, WM, WN, AVEC, BKIND, true>(P, batch, ncols, s);
   else launch_one<BM, BN, WM, WN, AVEC, BKIND, false>(P, batch, ncols, s);
+}
+
+template <int BM, int BN, int WM, int WN, bool SPLIT>
+static void launch_conv(const GemmDev& P, int nbatch, int T_out, hipStream_t s) {
+  const int tpb = (T_out + BM - 1) / BM;
+  dim3 grid(nbatch * tpb, (P.N + BN - 1) / BN, 1);
+  void* tok = prof_start(s);
+  hipLaunchKernelGGL((conv_kernel<BM, BN, WM, WN, SPLIT>), grid, dim3(256), 0, s, P, tpb, T_out);
+  if (tok) {
+    char name[128];
+    std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %s>", BM, BN, WM, WN,
+                  SPLIT ? "true" : "false");
+    prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
+  }
 }
 
 int gemm(const alcm_gemm_args& g, hipStream_t s) {
@@ -484,7 +683,20 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
     g_cost.flops = 2.0 * nb * (double)g.M * N * Kr;
     g_cost.bytes = nb * a_rows * g.a.C_in * 4.0 + bbytes + obytes;
   }
-  if (bkind == BK_W) {
+  const bool window_conv = bkind == BK_W && avec && batch == 1 && g.a.ksize > 1 && g.a.Cpad % 32 == 0 &&
+                           g.a.C_in == g.a.Cpad && (g.a.ksize - 1) * g.a.dil <= HALO_MAX &&
+                           g.out_rows_per_batch == g.a.rows_per_batch && g.M % g.a.rows_per_batch == 0 &&
+                           !g.disable_window;
+  if (window_conv) {
+    const int nb = g.M / g.a.rows_per_batch, T_out = g.a.rows_per_batch;
+    if (N <= 64) {
+      if (split) launch_conv<128, 64, 4, 1, true>(P, nb, T_out, s);
+      else launch_conv<128, 64, 4, 1, false>(P, nb, T_out, s);
+    } else {
+      if (split) launch_conv<128, 128, 2, 2, true>(P, nb, T_out, s);
+      else launch_conv<128, 128, 2, 2, false>(P, nb, T_out, s);
+    }
+  } else if (bkind == BK_W) {
     if (N <= 32) {
       if (avec) launch_split<256, 32, 4, 1, true, BK_W>(P, batch, N, split, s);
       else launch_split<256, 32, 4, 1, false, BK_W>(P, batch, N, split, s);

@@ -39,6 +39,7 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
 int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
+int amp_conv(const alcm_amp_args& a, hipStream_t s);
 
 bool prof_enabled();
 void* prof_start(hipStream_t s);

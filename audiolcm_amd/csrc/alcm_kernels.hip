@@ -160,86 +160,95 @@ int softmax_rows(float* x, int rows, int n, int64_t ld, hipStream_t s) {
 //   s[m]   = up[m] + inv_beta[c] * sin(up[m] * alpha_exp[c])^2
 //   out[j] = sum_k f_dn[k] * s[clamp(2j + k - 5, 0, 2T-1)]
 // Each thread owns one channel and R consecutive outputs; the input window x[j0-6, j0+R+6)
-// and the 2R+10 snake samples stay in registers.  Lanes run along channels (coalesced).
+// and the 2R+10 snake samples stay in registers (compile-time indices).  Lanes run along
+// channels (coalesced).  The 12+12 filter taps are kernel arguments (SGPR operands).
 constexpr int A1D_R = 16;
 constexpr int A1D_W = A1D_R + 12;
 constexpr int A1D_S = 2 * A1D_R + 10;
 
-template <bool EDGE>
-__device__ __forceinline__ void act1d_run(const float* __restrict__ xb, float* __restrict__ yb, int T, int64_t st,
-                                          int j0, float ea, float ib, const float* f_up, const float* f_dn) {
+struct Taps12 {
+  float up[12], dn[12];
+};
+
+// sin(x)^2 with a quadrant reduction (Cody-Waite, 3-term pi/2) and the cephes single-precision
+// minimax kernels on |r| <= pi/4: ~1 ulp for |x| < 1e4, no libm call, no branches.
+__device__ __forceinline__ float sin_sq(float x) {
+  const float k = rintf(x * 0.63661977236758134f);
+  float r = fmaf(-k, 1.5703125f, x);
+  r = fmaf(-k, 4.837512969970703125e-4f, r);
+  r = fmaf(-k, 7.54978995489188216e-8f, r);
+  const float z = r * r;
+  const float sn = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+  const float cs = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                  4.166664568298827e-2f), z, -0.5f), z, 1.0f);
+  const float v = (((int)k) & 1) ? cs : sn;
+  return v * v;
+}
+
+__device__ __forceinline__ float snake(float u, float ea, float ib) { return u + ib * sin_sq(u * ea); }
+
+// interior runs: every index compile-time, all values in registers
+__device__ __forceinline__ void act1d_run_interior(const float* __restrict__ xb, float* __restrict__ yb, int64_t st,
+                                                   int j0, float ea, float ib, const Taps12& f) {
   float win[A1D_W];
 #pragma unroll
-  for (int i = 0; i < A1D_W; ++i) {
-    int ti = j0 - 6 + i;
-    if (EDGE) ti = ti < 0 ? 0 : (ti > T - 1 ? T - 1 : ti);
-    win[i] = xb[(int64_t)ti * st];
-  }
+  for (int i = 0; i < A1D_W; ++i) win[i] = xb[(int64_t)(j0 - 6 + i) * st];
   float sv[A1D_S];
 #pragma unroll
   for (int q = 0; q < A1D_S; ++q) {
+    // m = 2*j0 - 5 + q; taps k == q (mod 2) read x[(m + 5 - k)/2] = win[(q - k)/2 + 6]
     float u = 0.f;
-    if (!EDGE) {
-      // m = 2*j0 - 5 + q; taps k with k == q (mod 2) read x[j0 + (q-k)/2 - 6 + 6] = win[(q-k)/2 + 6]
 #pragma unroll
-      for (int kk = 0; kk < 6; ++kk) {
-        const int k = 2 * kk + (q & 1);
-        u += f_up[k] * win[(q - k) / 2 + 6];
-      }
-    } else {
-      int m = 2 * j0 - 5 + q;
-      m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
-      const int par = (m & 1) ? 0 : 1;  // m even -> odd taps
-#pragma unroll
-      for (int kk = 0; kk < 6; ++kk) {
-        const int k = 2 * kk + par;
-        u += f_up[k] * win[(m + 5 - k) / 2 - (j0 - 6)];
-      }
+    for (int kk = 0; kk < 6; ++kk) {
+      const int k = 2 * kk + (q & 1);
+      u = fmaf(f.up[k], win[(q - k) / 2 + 6], u);
     }
-    u *= 2.0f;
-    const float sn = sinf(u * ea);
-    sv[q] = u + ib * (sn * sn);
+    sv[q] = snake(2.0f * u, ea, ib);
   }
 #pragma unroll
   for (int r = 0; r < A1D_R; ++r) {
-    const int j = j0 + r;
-    if (EDGE && j >= T) break;
     float o = 0.f;
 #pragma unroll
+    for (int k = 0; k < 12; ++k) o = fmaf(f.dn[k], sv[2 * r + k], o);
+    yb[(int64_t)(j0 + r) * st] = o;
+  }
+}
+
+// edge runs (sequence start/end, or T < R+12): direct evaluation with clamped indices, no arrays
+__device__ void act1d_run_edge(const float* __restrict__ xb, float* __restrict__ yb, int T, int64_t st, int j0,
+                               float ea, float ib, const Taps12& f) {
+  for (int j = j0; j < j0 + A1D_R && j < T; ++j) {
+    float o = 0.f;
     for (int k = 0; k < 12; ++k) {
-      int q = 2 * r + k;
-      if (EDGE) {
-        int m = 2 * j + k - 5;
-        m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
-        q = m - (2 * j0 - 5);
+      int m = 2 * j + k - 5;
+      m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+      float u = 0.f;
+      for (int kk = 0; kk < 6; ++kk) {
+        const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+        int xi = (m + 5 - ku) / 2;
+        xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+        u = fmaf(f.up[ku], xb[(int64_t)xi * st], u);
       }
-      o += f_dn[k] * sv[q];
+      o = fmaf(f.dn[k], snake(2.0f * u, ea, ib), o);
     }
     yb[(int64_t)j * st] = o;
   }
 }
 
-__global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int T,
-                                                    int C, int64_t sb, int64_t st, const float* __restrict__ aexp,
-                                                    const float* __restrict__ ibeta, const float* __restrict__ fup,
-                                                    const float* __restrict__ fdn, int runs, int64_t total) {
-  __shared__ float f_up[12], f_dn[12];
-  if (threadIdx.x < 12) {
-    f_up[threadIdx.x] = fup[threadIdx.x];
-    f_dn[threadIdx.x] = fdn[threadIdx.x];
-  }
-  __syncthreads();
-  for (int64_t w = blockIdx.x * (int64_t)256 + threadIdx.x; w < total; w += (int64_t)gridDim.x * 256) {
-    const int c = (int)(w % C);
-    const int64_t rb = w / C;
-    const int run = (int)(rb % runs);
-    const int b = (int)(rb / runs);
-    const int j0 = run * A1D_R;
+__global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x, float* __restrict__ y, int T, int C,
+                                                    int64_t sb, int64_t st, const float* __restrict__ aexp,
+                                                    const float* __restrict__ ibeta, const Taps12 f, int runs,
+                                                    uint32_t total, FastDiv cdiv, FastDiv rdiv) {
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < total; w += gridDim.x * 256u) {
+    uint32_t rb, c, b, run;
+    cdiv.divmod(w, rb, c);
+    rdiv.divmod(rb, b, run);
+    const int j0 = (int)run * A1D_R;
     const float* xb = x + (int64_t)b * sb + c;
     float* yb = y + (int64_t)b * sb + c;
-    const bool interior = (j0 >= 6) && (j0 + A1D_R + 6 <= T);
-    if (interior) act1d_run<false>(xb, yb, T, st, j0, aexp[c], ibeta[c], f_up, f_dn);
-    else act1d_run<true>(xb, yb, T, st, j0, aexp[c], ibeta[c], f_up, f_dn);
+    const float ea = aexp[c], ib = ibeta[c];
+    if (j0 >= 6 && j0 + A1D_R + 6 <= T) act1d_run_interior(xb, yb, st, j0, ea, ib, f);
+    else act1d_run_edge(xb, yb, T, st, j0, ea, ib, f);
   }
 }
 
@@ -250,13 +259,20 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
   if (x == y) return set_error(ALCM_E_INVALID, "activation1d: in-place not supported");
   const int runs = (T + A1D_R - 1) / A1D_R;
   const int64_t total = (int64_t)B * runs * C;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+  if (total >= (1ll << 31)) return set_error(ALCM_E_INVALID, "activation1d: problem too large");
+  Taps12 f;
+  for (int k = 0; k < 12; ++k) {
+    f.up[k] = up_filter[k];
+    f.dn[k] = down_filter[k];
+  }
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
   void* tok = prof_start(s);
-  hipLaunchKernelGGL(act1d_kernel, dim3(blocks), dim3(256), 0, s, x, y, B, T, C, sb, st, alpha_exp, inv_beta,
-                     up_filter, down_filter, runs, total);
+  hipLaunchKernelGGL(act1d_kernel, dim3(blocks), dim3(256), 0, s, x, y, T, C, sb, st, alpha_exp, inv_beta, f, runs,
+                     (uint32_t)total, FastDiv((uint32_t)C), FastDiv((uint32_t)runs));
   // per output sample: 12 up-FIR + 12 down-FIR MACs on 2 upsampled samples, 2 sin; 4 B in + 4 B out
-  prof_stop(tok, s, "alcm::act1d_kernel(float const*, float*, int, int, int, long, long, float const*, float const*, "
-            "float const*, float const*, int, long)", 2.0 * 36.0 * B * (double)T * C, 8.0 * B * (double)T * C);
+  prof_stop(tok, s, "alcm::act1d_kernel(float const*, float*, int, int, long, long, float const*, float const*, "
+            "alcm::Taps12, int, unsigned int, alcm::FastDiv, alcm::FastDiv)", 2.0 * 36.0 * B * (double)T * C,
+            8.0 * B * (double)T * C);
   ALCM_HIP(hipGetLastError());
   return 0;
 }
@@ -302,9 +318,13 @@ __global__ void sincos_embed_kernel(const float* __restrict__ v, float vscale, c
   const int b = blockIdx.x;
   for (int i = threadIdx.x; i < half; i += blockDim.x) {
     const float a = (v[b] * vscale) * freqs[i];
-    // arguments reach ~4e3 rad: evaluate sin/cos of the fp32 argument in fp64 so the result is the
-    // correctly rounded value the reference's CPU libm returns (fp32 OCML differs by up to 3e-5 here)
-    const float sn = (float)sin((double)a), cs = (float)cos((double)a);
+    // arguments reach ~4e3 rad: reduce modulo 2*pi in fp64 (exact enough for |a| < 1e6), then fp32
+    // sin/cos on |r| <= pi, matching the reference CPU libm to ~1 ulp (fp32 OCML on the raw argument
+    // differed by up to 3e-5 here)
+    const double ad = (double)a;
+    const double kq = rint(ad * 0.15915494309189535);
+    const float r = (float)(ad - kq * 6.283185307179586);
+    const float sn = sinf(r), cs = cosf(r);
     out[(int64_t)b * 2 * half + i] = cos_first ? cs : sn;
     out[(int64_t)b * 2 * half + half + i] = cos_first ? sn : cs;
   }

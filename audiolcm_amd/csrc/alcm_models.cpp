@@ -77,8 +77,7 @@ struct VaeW {
 struct ActW {
   float* aexp = nullptr;
   float* ibeta = nullptr;
-  float* fup = nullptr;
-  float* fdn = nullptr;
+  float fup[12] = {0}, fdn[12] = {0};  // host copies: the kernel takes the taps as arguments
 };
 struct AmpW {
   int k = 3;
@@ -367,8 +366,10 @@ static ActW build_act(Ingest& I, const std::string& p, int C) {
   a.ibeta = I.upload(be);
   auto fu = I.get(p + "upsample.filter", {1, 1, 12});
   auto fd = I.get(p + "downsample.lowpass.filter", {1, 1, 12});
-  a.fup = I.upload(fu);
-  a.fdn = I.upload(fd);
+  for (int k = 0; k < 12; ++k) {
+    a.fup[k] = fu[k];
+    a.fdn[k] = fd[k];
+  }
   return a;
 }
 
@@ -870,6 +871,22 @@ static int act1d(hipStream_t s, const ActW& a, const float* x, float* y, int B, 
   return activation1d(x, y, B, T, C, (int64_t)T * C, C, a.aexp, a.ibeta, a.fup, a.fdn, s);
 }
 
+static bool amp_fusable(int c) { return c == 24 || c == 48 || c == 96; }
+
+// fused Activation1d + conv (alcm_ampconv.hip) for the narrow BigVGAN stages
+static int amp(hipStream_t s, int split, const ActW& a, const ConvW& w, const float* x, float* out, int B, int T,
+               int dil, const float* res, float out_scale, int accumulate, int out_act) {
+  alcm_amp_args g;
+  std::memset(&g, 0, sizeof(g));
+  g.x = x; g.B = B; g.T = T; g.Cin = w.w.cin;
+  g.act = 1; g.alpha_exp = a.aexp; g.inv_beta = a.ibeta; g.up_filter = a.fup; g.down_filter = a.fdn;
+  g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.Cout = w.w.rows; g.ksize = w.w.taps; g.dil = dil;
+  g.pad = (w.w.taps * dil - dil) / 2;
+  g.bias = w.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate; g.out_scale = out_scale;
+  g.split = split;
+  return amp_conv(g, s);
+}
+
 static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, int M, void* ws, size_t wsb,
                            hipStream_t s) {
   const VocW& G = m->voc;
@@ -906,6 +923,16 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
       const float* cur = u;
+      if (amp_fusable(S.cout)) {
+        for (size_t l = 0; l < A.dil.size(); ++l) {
+          const bool last = l + 1 == A.dil.size();
+          ALCM_TRY(amp(s, split, A.act[2 * l], A.c1[l], cur, y, B, To, A.dil[l], nullptr, 1.f, 0, 0));
+          ALCM_TRY(amp(s, split, A.act[2 * l + 1], A.c2[l], y, last ? x : rb, B, To, 1, cur, last ? inv : 1.f,
+                       last && j > 0, 0));
+          cur = rb;
+        }
+        continue;
+      }
       for (size_t l = 0; l < A.dil.size(); ++l) {
         ALCM_TRY(act1d(s, A.act[2 * l], cur, w.a, B, To, S.cout));
         ConvOpts o1;
@@ -928,6 +955,8 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     T = To;
   }
   // activation_post -> conv_post k7 -> tanh (models.py:201-203)
+  if (amp_fusable(G.st.back().cout))
+    return amp(s, split, G.post_act, G.post, x, wav, B, T, 1, nullptr, 1.f, 0, ACT_TANH);
   ALCM_TRY(act1d(s, G.post_act, x, w.a, B, T, G.st.back().cout));
   ConvOpts o;
   o.pad = 3;

@@ -78,7 +78,7 @@ def gemm(args: _hip.GemmArgs) -> None:
 def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, padding: int = 0,
            dilation: int = 1, upsample: int = 1, split: bool = True, channels_last: bool = False,
            act: int = 0, residual: Optional[torch.Tensor] = None, packed: Optional[PackedWeight] = None,
-           prologue: Optional[dict] = None) -> torch.Tensor:
+           prologue: Optional[dict] = None, window: bool = True) -> torch.Tensor:
     """F.conv1d(x, w, bias, padding=padding, dilation=dilation) on the MFMA implicit GEMM.
 
     x is (B, Cin, T) (reference NCT layout) or, with channels_last, (B, T, Cin); the result
@@ -127,6 +127,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     g.out = ptr(out)
     g.out_rows_per_batch, g.out_step, g.out_off = Tout, 1, 0
     g.split = int(split)
+    g.disable_window = int(not window)
     gemm(g)
     return out
 
@@ -270,9 +271,11 @@ def activation1d(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor, up
     x_cl = x_cl.contiguous()
     ae, ib = snake_params(alpha, beta)
     y = torch.empty_like(x_cl)
+    fu = up_filter.detach().reshape(-1).float().cpu().contiguous()
+    fd = down_filter.detach().reshape(-1).float().cpu().contiguous()
     check(lib().alcm_activation1d(ptr(x_cl), ptr(y), B, T, Cc, T * Cc, Cc, ptr(ae.contiguous()),
-                                  ptr(ib.contiguous()), ptr(up_filter.reshape(-1).contiguous()),
-                                  ptr(down_filter.reshape(-1).contiguous()), stream_handle()), "activation1d")
+                                  ptr(ib.contiguous()), fu.data_ptr(), fd.data_ptr(), stream_handle()),
+          "activation1d")
     return y
 
 
@@ -293,4 +296,35 @@ def sincos_embedding(v: torch.Tensor, freqs: torch.Tensor, scale: float, cos_fir
     out = torch.empty((B, 2 * half), device=v.device, dtype=torch.float32)
     check(lib().alcm_sincos_embedding(ptr(v.float().contiguous()), scale, ptr(freqs), B, half, int(cos_first),
                                       ptr(out), stream_handle()), "sincos_embedding")
+    return out
+
+
+def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int, padding: int,
+             act: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]] = None,
+             residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
+             accumulate_into: Optional[torch.Tensor] = None, split: bool = True) -> torch.Tensor:
+    """Fused conv_{k,d}(Activation1d(x)) on channels-last (B, T, C) for C in {24, 48, 96}.
+
+    act = (alpha, beta, up_filter, down_filter) of the SnakeBeta Activation1d (None: no activation)."""
+    B, T, Cin = x_cl.shape
+    x_cl = x_cl.contiguous()
+    pw = pack_conv_weight(w)
+    a = _hip.AmpArgs()
+    a.x, a.B, a.T, a.Cin = ptr(x_cl), B, T, Cin
+    keep = []
+    if act is not None:
+        ae, ib = snake_params(act[0], act[1])
+        ae, ib = ae.contiguous(), ib.contiguous()
+        fu = act[2].detach().reshape(-1).float().cpu().contiguous()
+        fd = act[3].detach().reshape(-1).float().cpu().contiguous()
+        keep += [ae, ib, fu, fd]
+        a.act, a.alpha_exp, a.inv_beta, a.up_filter, a.down_filter = 1, ptr(ae), ptr(ib), fu.data_ptr(), fd.data_ptr()
+    a.w, a.w_lo_off, a.kpad, a.Cout, a.ksize, a.dil, a.pad = ptr(pw.data), pw.lo_off, pw.kpad, pw.rows, pw.taps, \
+        dilation, padding
+    a.bias = ptr(bias)
+    a.res = ptr(residual.contiguous()) if residual is not None else None
+    out = accumulate_into if accumulate_into is not None else torch.empty((B, T, pw.rows), device=x_cl.device)
+    a.out, a.out_act, a.accumulate, a.out_scale, a.split = ptr(out), out_act, int(accumulate_into is not None), \
+        out_scale, int(split)
+    check(lib().alcm_amp_conv(C.byref(a), stream_handle()), "amp_conv")
     return out

@@ -97,6 +97,7 @@ typedef struct alcm_gemm_args {
   int64_t o_sb, o_st, o_sc, o_zs1, o_zs2;
   int out_rows_per_batch, out_step, out_off;
   int split;
+  int disable_window; /* 1: never use the window-conv kernel (testing / A-B timing) */
 } alcm_gemm_args;
 
 int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream);
@@ -118,9 +119,35 @@ int alcm_layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, c
                     const float* beta, const float* add, int64_t ld_add, float* y, int64_t ld_out,
                     alcm_stream_t stream);
 int alcm_softmax_rows(float* x, int rows, int n, int64_t ld, alcm_stream_t stream);
+/* fused Activation1d(SnakeBeta): x,y DEVICE (b,t,c) channels-last, not in place; alpha_exp = exp(alpha),
+ * inv_beta = 1/(exp(beta)+1e-9) per channel (DEVICE); up_filter/down_filter: HOST arrays of 12 taps */
 int alcm_activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st,
                       const float* alpha_exp, const float* inv_beta, const float* up_filter,
                       const float* down_filter, alcm_stream_t stream);
+
+/* fused BigVGAN narrow-stage layer (C = 24/48/96): y = conv_{k,dil}(Activation1d(x)) + bias, then
+ * optional out_act (ACT_TANH for conv_post), + res, * out_scale, + out (accumulate).
+ * x (B,T,Cin), res/out (B,T,Cout) channels-last DEVICE; w packed as alcm_pack_conv_weight
+ * (cpad = Cin); act=0 skips the activation; filters are HOST arrays of 12 taps. */
+typedef struct alcm_amp_args {
+  const float* x;
+  int B, T, Cin;
+  int act;
+  const float* alpha_exp;
+  const float* inv_beta;
+  const float* up_filter;
+  const float* down_filter;
+  const void* w;
+  int64_t w_lo_off;
+  int kpad, Cout, ksize, dil, pad;
+  const float* bias;
+  const float* res;
+  float* out;
+  int out_act, accumulate;
+  float out_scale;
+  int split;
+} alcm_amp_args;
+int alcm_amp_conv(const alcm_amp_args* args, alcm_stream_t stream);
 
 /* ---------------------------------------------------------------- LCM scheduler pieces */
 /* coeffs (HOST array of 6): {sqrt_a, sqrt_b, c_out, c_skip, sqrt_a_prev, sqrt_b_prev};

@@ -42,6 +42,9 @@ def dev(t):
     (2, 20, 33, 576, 5, 2, 1, False),    # DiT proj_in: 20 channels (padded K)
     (1, 24, 64, 1, 7, 3, 1, True),       # conv_post: N=1
     (2, 80, 16, 1536, 7, 3, 1, False),   # conv_pre from NCT mel
+    (2, 96, 300, 130, 11, 25, 5, True),  # window-conv: k11 d5, 3 row tiles per batch, ragged N
+    (3, 64, 129, 48, 7, 9, 3, True),     # window-conv, BN=64 tile, T not a tile multiple
+    (1, 32, 5, 64, 3, 1, 1, True),       # window-conv, T shorter than the halo
 ])
 @pytest.mark.parametrize("split", [True, False])
 def test_conv1d(K, B, Cin, T, Cout, k, pad, dil, cl, split):
@@ -55,6 +58,17 @@ def test_conv1d(K, B, Cin, T, Cout, k, pad, dil, cl, split):
         y = y.permute(0, 2, 1)
     assert y.shape == ref.shape
     assert rel_l2(y.numpy(), ref.numpy()) < (SPLIT_TOL if split else BF16_TOL)
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_window_conv_matches_tap_loader(K, split):
+    """The window-conv kernel and the tap-by-tap implicit GEMM give the same result (same bf16 operands)."""
+    x = _r((2, 300, 128), 40)
+    w = _r((192, 128, 7), 41, 0.03)
+    b = _r((192,), 42, 0.1)
+    y1 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, split=split, channels_last=True)
+    y2 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, split=split, channels_last=True, window=False)
+    assert rel_l2(y1.cpu().numpy(), y2.cpu().numpy()) < (1e-6 if split else 1e-5)
 
 
 def test_conv1d_upsample_nearest(K):
@@ -160,6 +174,67 @@ def test_activation1d_long(K):
     ref = O.activation1d(x, a, b, f, f)
     y = K.activation1d(dev(x.permute(0, 2, 1).contiguous()), dev(a), dev(b), dev(f), dev(f)).cpu().permute(0, 2, 1)
     np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=2e-5, atol=5e-6)
+
+
+@pytest.mark.parametrize("C,k,dil,T,act,res", [
+    (24, 11, 5, 700, True, True), (48, 7, 3, 333, True, False), (96, 3, 1, 150, True, True),
+    (96, 11, 1, 40, False, False), (24, 3, 1, 5, True, True)])
+@pytest.mark.parametrize("split", [True, False])
+def test_amp_conv_fused(K, C, k, dil, T, act, res, split):
+    """Fused Activation1d + conv (BigVGAN narrow stages) vs oracle Activation1d then F.conv1d (+ residual)."""
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B = 2
+    x = _r((B, C, T), 50, 1.2)
+    a, bt = _r((C,), 51, 0.3), _r((C,), 52, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    w, bias = _r((C, C, k), 53, 0.7 / np.sqrt(C * k)), _r((C,), 54, 0.05)
+    r = _r((B, C, T), 55)
+    h = O.activation1d(x, a, bt, f, f) if act else x
+    ref = F.conv1d(h, w, bias, dilation=dil, padding=(k * dil - dil) // 2) + (r if res else 0)
+    y = K.amp_conv(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(bias), dil, (k * dil - dil) // 2,
+                   act=(dev(a), dev(bt), f, f) if act else None,
+                   residual=dev(r.permute(0, 2, 1).contiguous()) if res else None, split=split).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if split else BF16_TOL)
+
+
+def test_amp_conv_post_tanh_and_accumulate(K):
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    x = _r((2, 24, 257), 56)
+    a, bt = _r((24,), 57, 0.3), _r((24,), 58, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    w, bias = _r((1, 24, 7), 59, 0.2), _r((1,), 60, 0.05)
+    ref = torch.tanh(F.conv1d(O.activation1d(x, a, bt, f, f), w, bias, padding=3))
+    y = K.amp_conv(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(bias), 1, 3, act=(dev(a), dev(bt), f, f),
+                   out_act=4).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < 3e-5
+    acc = dev(torch.ones((2, 257, 1)))
+    K.amp_conv(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(bias), 1, 3, act=(dev(a), dev(bt), f, f),
+               out_act=4, out_scale=0.5, accumulate_into=acc)
+    assert rel_l2(acc.cpu().permute(0, 2, 1).numpy(), (1 + 0.5 * ref).numpy()) < 3e-5
+
+
+def test_embedding_diagnostic(K):
+    """Prints where the device timestep embedding differs from the reference (diagnostic, never fails)."""
+    from audiolcm_amd import schedule
+    g = golden("schedule.npz")
+    t = torch.from_numpy(g["t"])
+    f = schedule.timestep_freqs()
+    te = K.sincos_embedding(dev(t.float()), dev(f), 1.0, True).cpu().numpy()
+    d = np.abs(te - g["timestep_emb"])
+    idx = np.argwhere(d > 2e-6)
+    args = (t[:, None].float() * f[None]).numpy()
+    for bi, i in idx[:6]:
+        col = i % 128
+        print("EMBDIAG", int(t[bi]), int(i), float(args[bi, col]), float(te[bi, i]), float(g["timestep_emb"][bi, i]))
+    ones = torch.ones(1)
+    direct = K.sincos_embedding(dev(torch.from_numpy(args[0, 10:16].copy())), dev(ones), 1.0, True).cpu().numpy()
+    print("EMBDIAG direct-arg cos", direct[:, 0].tolist(), "ref", g["timestep_emb"][0, 10:16].tolist())
+    prod = K.sincos_embedding(dev(torch.tensor([999.0])), dev(f[10:16].contiguous()), 1.0, True).cpu().numpy()
+    print("EMBDIAG product-path cos", prod[0, :6].tolist())
+    tg = torch.cos(dev(torch.from_numpy(args))).cpu().numpy()
+    print("EMBDIAG torch-gpu-cos max err", float(np.abs(tg - g["timestep_emb"][:, :128]).max()))
 
 
 def test_lcm_step_golden(K):
