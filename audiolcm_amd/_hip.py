@@ -38,7 +38,7 @@ class GemmArgs(C.Structure):
                 ("r_sb", i64), ("r_st", i64), ("r_sc", i64), ("r_zs1", i64), ("r_zs2", i64), ("out", fp),
                 ("o_sb", i64), ("o_st", i64), ("o_sc", i64), ("o_zs1", i64), ("o_zs2", i64),
                 ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("split", C.c_int),
-                ("disable_window", C.c_int)]
+                ("disable_window", C.c_int), ("tile_n", C.c_int)]
 
 
 class AmpArgs(C.Structure):

@@ -140,14 +140,13 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
     const int c = e % P.Cin, run = e / P.Cin;
     float o[AR];
     act_run<ACT>(xb + c, P.Cin, P.T, tb, run * AR, WR, ACT ? P.aexp[c] : 0.f, ACT ? P.ibeta[c] : 0.f, P.f, o);
+    // rows in [WR, runs*AR) are never read by the MFMAs; WR_MAX covers them, so no per-row guard
 #pragma unroll
     for (int r = 0; r < AR; ++r) {
       const int w = run * AR + r;
-      if (w < WR) {
-        const __bf16 h = (__bf16)o[r];
-        Wn[0][w * S + c] = h;
-        if (SPLIT) Wn[NP - 1][w * S + c] = (__bf16)(o[r] - (float)h);
-      }
+      const __bf16 h = (__bf16)o[r];
+      Wn[0][w * S + c] = h;
+      if (SPLIT) Wn[NP - 1][w * S + c] = (__bf16)(o[r] - (float)h);
     }
   }
   __syncthreads();

@@ -689,7 +689,9 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
                            !g.disable_window;
   if (window_conv) {
     const int nb = g.M / g.a.rows_per_batch, T_out = g.a.rows_per_batch;
-    if (N <= 64) {
+    // 64-wide N tiles when 128-wide tiles would waste a third of the MFMA work (N = 192, 320, ...)
+    const bool narrow = g.tile_n == 64 || (g.tile_n == 0 && (N <= 64 || (N % 128 != 0 && N % 64 == 0)));
+    if (narrow) {
       if (split) launch_conv<128, 64, 4, 1, true>(P, nb, T_out, s);
       else launch_conv<128, 64, 4, 1, false>(P, nb, T_out, s);
     } else {

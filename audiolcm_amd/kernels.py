@@ -78,7 +78,7 @@ def gemm(args: _hip.GemmArgs) -> None:
 def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, padding: int = 0,
            dilation: int = 1, upsample: int = 1, split: bool = True, channels_last: bool = False,
            act: int = 0, residual: Optional[torch.Tensor] = None, packed: Optional[PackedWeight] = None,
-           prologue: Optional[dict] = None, window: bool = True) -> torch.Tensor:
+           prologue: Optional[dict] = None, window: bool = True, tile_n: int = 0) -> torch.Tensor:
     """F.conv1d(x, w, bias, padding=padding, dilation=dilation) on the MFMA implicit GEMM.
 
     x is (B, Cin, T) (reference NCT layout) or, with channels_last, (B, T, Cin); the result
@@ -128,6 +128,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     g.out_rows_per_batch, g.out_step, g.out_off = Tout, 1, 0
     g.split = int(split)
     g.disable_window = int(not window)
+    g.tile_n = tile_n
     gemm(g)
     return out
 

@@ -69,17 +69,26 @@ def step_coeffs(t: int, prev_t: int, ac: torch.Tensor, timestep_scaling: float =
     return [float(torch.as_tensor(v, dtype=torch.float32)) for v in vals]
 
 
+def _cr_exp(x32: torch.Tensor) -> torch.Tensor:
+    """Correctly rounded fp32 exp of an fp32 tensor.  torch's CPU exp is platform dependent in the
+    last ulp (AVX2 vs AVX-512 SLEEF paths differ on ~3% of these entries); the correctly rounded value
+    makes the tables identical on every host."""
+    return torch.from_numpy(np.exp(x32.numpy().astype(np.float64)).astype(np.float32))
+
+
 def guidance_freqs(embedding_dim: int = 256) -> torch.Tensor:
-    """exp(-ln(1e4)/(half-1) * i), fp32 exactly as get_guidance_scale_embedding (scheduling_lcm.py:103-105)."""
+    """exp(-ln(1e4)/(half-1) * i) (scheduling_lcm.py:103-105): the fp32 exponent exactly as the
+    reference computes it, exp correctly rounded."""
     half = embedding_dim // 2
     emb = torch.log(torch.tensor(10000.0)) / (half - 1)
-    return torch.exp(torch.arange(half, dtype=torch.float32) * -emb)
+    return _cr_exp(torch.arange(half, dtype=torch.float32) * -emb)
 
 
 def timestep_freqs(dim: int = 256, max_period: int = 10000) -> torch.Tensor:
-    """exp(-ln(max_period) * i / half), fp32 exactly as TimestepEmbedder (concatDiT.py:60-62)."""
+    """exp(-ln(max_period) * i / half) (concatDiT.py:60-62): fp32 exponent as the reference, exp
+    correctly rounded."""
     half = dim // 2
-    return torch.exp(-math.log(max_period) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
+    return _cr_exp(-math.log(max_period) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
 
 
 def sample_plan(S: int, original_inference_steps: int = 50, timesteps: Optional[Sequence[int]] = None

@@ -98,6 +98,7 @@ typedef struct alcm_gemm_args {
   int out_rows_per_batch, out_step, out_off;
   int split;
   int disable_window; /* 1: never use the window-conv kernel (testing / A-B timing) */
+  int tile_n;         /* 0: automatic; 64 / 128: force the N tile of the window-conv kernel */
 } alcm_gemm_args;
 
 int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream);

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmarks on BigVGAN / DiT shapes (B=32), timed with torch CUDA events.
+
+Used to A/B kernel variants in one process and as the target of rocprofv3 PMC passes:
+    python scripts/microbench.py amp        # fused Activation1d+conv, C=24/48/96
+    python scripts/microbench.py conv       # window conv, BigVGAN stage 0-2 / VAE / DiT FFN shapes
+    python scripts/microbench.py act        # standalone Activation1d
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from audiolcm_amd import _hip, kernels as K  # noqa: E402
+from audiolcm_amd.recipe import kaiser_sinc_filter1d  # noqa: E402
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def bench_amp(B=32):
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T in ((24, 159744), (48, 79872), (96, 39936)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        for k, d in ((11, 5), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            bias = torch.randn(C, device="cuda") * 0.05
+            for split in (True, False):
+                for act in (True, False):
+                    ms = timeit(lambda: K.amp_conv(x, w, bias, d, (k * d - d) // 2,
+                                                   act=(a, bt, f, f) if act else None, residual=r, split=split))
+                    gb = B * T * C * 4 * 3 / 1e9
+                    tf = 2 * B * T * C * C * k / 1e12
+                    print(f"amp C={C:3d} k={k:2d} d={d} split={int(split)} act={int(act)}: {ms:7.3f} ms "
+                          f"{gb / ms:6.2f} TB/s {tf / ms * 1e3:7.1f} TF/s")
+
+
+def bench_conv(B=32):
+    cases = [("bigvgan s0 k11d5", 2496, 768, 768, 11, 5), ("bigvgan s1 k7d3", 9984, 384, 384, 7, 3),
+             ("bigvgan s2 k3d1", 19968, 192, 192, 3, 1), ("dit ffn0 k9", 467, 576, 4608, 9, 1),
+             ("dit ffn2 k9", 467, 2304, 576, 9, 1), ("vae k3 1536", 312, 1536, 1536, 3, 1)]
+    for name, T, Cin, Cout, k, d in cases:
+        x = torch.randn((B, T, Cin), device="cuda")
+        w = torch.randn((Cout, Cin, k), device="cuda") * (1 / (Cin * k) ** 0.5)
+        pw = K.pack_conv_weight(w)
+        for split in (True, False):
+            for window, tn in ((True, 0), (True, 64), (True, 128), (False, 0)):
+                ms = timeit(lambda: K.conv1d(x, w, None, padding=(k * d - d) // 2, dilation=d, split=split,
+                                             channels_last=True, packed=pw, window=window, tile_n=tn), reps=3)
+                tf = 2 * B * T * Cin * Cout * k / 1e12
+                print(f"conv {name:18s} split={int(split)} window={int(window)} tn={tn:3d}: {ms:8.3f} ms "
+                      f"{tf / ms * 1e3:7.1f} TF/s algorithmic ({tf / ms * 1e3 * (3 if split else 1) / 2500:5.1%} "
+                      f"of 2.5 PF MFMA)")
+
+
+def bench_act(B=32):
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T in ((768, 2496), (384, 9984), (24, 159744)):
+        x = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        ms = timeit(lambda: K.activation1d(x, a, bt, f, f))
+        print(f"act1d C={C} T={T}: {ms:.3f} ms {B * T * C * 8 / 1e9 / ms:.2f} TB/s")
+
+
+if __name__ == "__main__":
+    _hip.require_device(0)
+    which = sys.argv[1:] or ["amp", "conv", "act"]
+    for w in which:
+        {"amp": bench_amp, "conv": bench_conv, "act": bench_act}[w]()

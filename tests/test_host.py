@@ -2,6 +2,7 @@
 
 No compute runs here: the HIP library is only loaded and its exports checked.
 """
+import math
 import os
 import re
 import subprocess
@@ -54,14 +55,18 @@ def test_sample_plan():
 
 
 def test_frequency_tables_match_reference():
-    from oracle import alcm_oracle as O
+    """Tables equal the reference's up to the last ulp of exp (platform dependent in torch itself):
+    at t = 999 / w*1000 = 4000 one ulp of a frequency moves the embedding by <= 3e-5 / 3e-4."""
     g = golden("schedule.npz")
     t = torch.from_numpy(g["t"])
+    ref_t = torch.exp(-math.log(10000) * torch.arange(0, 128, dtype=torch.float32) / 128)
+    assert (schedule.timestep_freqs() - ref_t).abs().max() <= 1.2e-7 * ref_t.abs().max()
     args = t[:, None].float() * schedule.timestep_freqs()[None]
-    np.testing.assert_array_equal(torch.cat([torch.cos(args), torch.sin(args)], 1).numpy(), g["timestep_emb"])
+    np.testing.assert_allclose(torch.cat([torch.cos(args), torch.sin(args)], 1).numpy(), g["timestep_emb"],
+                               atol=5e-5)
     w = torch.tensor(4).repeat(3) * 1000.0
     a = w[:, None] * schedule.guidance_freqs()[None]
-    np.testing.assert_array_equal(torch.cat([torch.sin(a), torch.cos(a)], 1).numpy(), g["guidance_w4"])
+    np.testing.assert_allclose(torch.cat([torch.sin(a), torch.cos(a)], 1).numpy(), g["guidance_w4"], atol=3e-4)
 
 
 def test_recipe_keys_and_shapes():
