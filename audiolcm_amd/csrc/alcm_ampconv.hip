@@ -118,9 +118,13 @@ __device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st
 }
 
 // BM output rows per workgroup (4 waves x BM/4 rows), all Cout (<= TN*16) columns.
+constexpr int AMP_WAVES = 8;  // 512-thread workgroups: one activation item per thread, more waves in flight
 template <int BM, int TN, int CPAD, bool SPLIT, bool ACT>
-__global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
-  constexpr int TM = BM / 64;
+__global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P) {
+  constexpr int NT = 64 * AMP_WAVES;
+  constexpr int WROWS = BM / AMP_WAVES;  // output rows per wave
+  constexpr int TM = WROWS / 16;
+  static_assert(TM >= 1 && WROWS % 16 == 0, "BM must give each wave a multiple of 16 rows");
   constexpr int S = CPAD + 8 + ((8 - (CPAD + 8) % 32 + 32) % 32);  // row stride (bf16) == 8 mod 32
   constexpr int WR_MAX = BM + 64;
   constexpr int NP = SPLIT ? 2 : 1;
@@ -136,7 +140,22 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
   // ---- 1. activation window -> LDS (bf16 hi/lo)
   const int runs = (WR + AR - 1) / AR;
   const int items = runs * P.Cin;
-  for (int e = tid; e < items; e += 256) {
+  // residual of this lane's output elements: issued before the activation phase so its latency hides
+  float resv[TM][4][TN];
+  {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = t0 + wave * WROWS + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = j * 16 + (lane & 15);
+          resv[i][r][j] = (P.res && t < P.T && n < P.Cout) ? P.res[(int64_t)b * P.r_sb + (int64_t)t * P.Cout + n] : 0.f;
+        }
+      }
+  }
+  for (int e = tid; e < items; e += NT) {
     const int c = e % P.Cin, run = e / P.Cin;
     float o[AR];
     act_run<ACT>(xb + c, P.Cin, P.T, tb, run * AR, WR, ACT ? P.aexp[c] : 0.f, ACT ? P.ibeta[c] : 0.f, P.f, o);
@@ -153,7 +172,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
 
   // ---- 2. implicit GEMM over K = (tap, channel), A from the window, B straight from global
   const int Kr = P.ksize * CPAD;
-  const int row_base = wave * (BM / 4) + (lane & 15);
+  const int row_base = wave * WROWS + (lane & 15);
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -224,7 +243,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
   for (int i = 0; i < TM; ++i) {
 #pragma clang loop unroll(full)
     for (int r = 0; r < 4; ++r) {
-      const int t = t0 + wave * (BM / 4) + i * 16 + (lane >> 4) * 4 + r;
+      const int t = t0 + wave * WROWS + i * 16 + (lane >> 4) * 4 + r;
       if (t >= P.T) continue;
 #pragma clang loop unroll(full)
       for (int j = 0; j < TN; ++j) {
@@ -233,7 +252,7 @@ __global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
         float v = acc[i][j][r];
         if (P.bias) v += P.bias[n];
         if (P.out_act) v = alcm_act(v, P.out_act);
-        if (P.res) v += P.res[(int64_t)b * P.r_sb + (int64_t)t * P.Cout + n];
+        v += resv[i][r][j];
         v *= P.out_scale;
         float* o = P.out + (int64_t)b * P.o_sb + (int64_t)t * P.Cout + n;
         if (P.accumulate) v += *o;
@@ -250,11 +269,11 @@ static void launch_amp(const AmpDev& P, int B, bool split, bool act, hipStream_t
   dim3 grid(B * Q.tiles_per_batch);
   void* tok = prof_start(s);
   if (split) {
-    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, true>), grid, dim3(256), 0, s, Q);
-    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, false>), grid, dim3(256), 0, s, Q);
+    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
+    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
   } else {
-    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, true>), grid, dim3(256), 0, s, Q);
-    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, false>), grid, dim3(256), 0, s, Q);
+    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
+    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
   }
   if (tok) {
     char name[128];

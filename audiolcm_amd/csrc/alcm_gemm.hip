@@ -27,7 +27,19 @@
 namespace alcm {
 
 constexpr int BK = 32;
-constexpr int LDS_ROW = 40;  // bf16 per LDS row: 32 + 8 pad (80 B) -> ds_read_b128 aligned, fewer conflicts
+// GEMM tiles in LDS: rows of BK=32 bf16 (64 B, unpadded); the 16-B chunk kq of row r sits at chunk
+// slot kq ^ ((r >> 2) & 2).  A ds_read_b128 fragment read (lane l: row l&15 of an aligned 16-row
+// block, chunk l>>4) then hits 16 distinct 16-B bank slots in each of its four 16-lane groups
+// ({0-3,12-15,20-27}, ...), i.e. it is conflict-free; the 80-B padded rows used before were 2-way.
+constexpr int LDS_ROW = 32;
+__device__ __forceinline__ int lds_off(int r, int kq) { return r * LDS_ROW + ((kq ^ ((r >> 2) & 2)) << 3); }
+// Conv input window rows: 48 bf16 (96 B).  Fragment reads start at any row (offset tap*dil), so the
+// layout must be conflict-free under translation: a 6-slot row stride is (16 rows x 4 chunks land on
+// distinct slots per lane group for every start row), unlike 4 (64 B) or 5 (80 B).
+constexpr int AW_ROW = 48;
+
+// Prologue activation: the path only fuses SiLU (GroupNorm/LayerNorm + swish) into operand loads.
+__device__ __forceinline__ float pro_act(float x, int act) { return act == ACT_SILU ? x / (1.0f + expf(-x)) : x; }
 
 struct ActDev {
   const float* p;
@@ -162,7 +174,7 @@ struct ActTile {
       if (A.pact) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (VEC || ci + j < A.C_in) v[i][j] = alcm_act(v[i][j], A.pact);
+          if (VEC || ci + j < A.C_in) v[i][j] = pro_act(v[i][j], A.pact);
       }
     }
   }
@@ -172,7 +184,7 @@ struct ActTile {
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       if (c >= CHUNKS) continue;
-      const int off = (c >> 2) * LDS_ROW + (c & 3) * 8;
+      const int off = lds_off(c >> 2, c & 3);
       split_store(v[i], hi + off, lo + off, SPLIT);
     }
   }
@@ -205,7 +217,7 @@ struct ActTTile {
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       if (c >= CHUNKS) continue;
-      const int off = (c % ROWS) * LDS_ROW + (c / ROWS) * 8;
+      const int off = lds_off(c % ROWS, c / ROWS);
       split_store(v[i], hi + off, lo + off, SPLIT);
     }
   }
@@ -217,17 +229,25 @@ struct WTile {
   static constexpr int CHUNKS = ROWS * 4;
   static constexpr int PER = (CHUNKS + 255) / 256;
   uint4 h[PER], l[PER];
-  __device__ __forceinline__ void load(const WDev& W, int tid, int row0, int k0, bool split) {
+  const u16* src[PER];
+  bool ok[PER];
+  __device__ __forceinline__ void init(const WDev& W, int tid, int row0) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       const int r = row0 + (c >> 2);
+      ok[i] = c < CHUNKS && r < W.rows;
+      src[i] = W.p + (int64_t)(ok[i] ? r : 0) * W.Kpad + (c & 3) * 8;
+    }
+  }
+  __device__ __forceinline__ void load(const WDev& W, int k0, bool split) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
       h[i] = make_uint4(0, 0, 0, 0);
       l[i] = make_uint4(0, 0, 0, 0);
-      if (c < CHUNKS && r < W.rows) {
-        const u16* src = W.p + (int64_t)r * W.Kpad + k0 + (c & 3) * 8;
-        h[i] = *reinterpret_cast<const uint4*>(src);
-        if (split) l[i] = *reinterpret_cast<const uint4*>(src + W.lo);
+      if (ok[i]) {
+        h[i] = *reinterpret_cast<const uint4*>(src[i] + k0);
+        if (split) l[i] = *reinterpret_cast<const uint4*>(src[i] + k0 + W.lo);
       }
     }
   }
@@ -237,7 +257,7 @@ struct WTile {
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       if (c >= CHUNKS) continue;
-      const int off = (c >> 2) * LDS_ROW + (c & 3) * 8;
+      const int off = lds_off(c >> 2, c & 3);
       *reinterpret_cast<uint4*>(hi + off) = h[i];
       if (SPLIT) *reinterpret_cast<uint4*>(lo + off) = l[i];
     }
@@ -268,10 +288,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
   WTile<BN> bt_w;
   if constexpr (BKIND == BK_ACT) bt_act.init(P.bact, tid, col0, zoff(P.zdiv, z, P.bact.zs1, P.bact.zs2));
   if constexpr (BKIND == BK_ACTT) bt_t.init(P.bT, tid, col0, zoff(P.zdiv, z, P.bT.zs1, P.bT.zs2));
+  if constexpr (BKIND == BK_W) bt_w.init(P.w, tid, col0);
 
   auto load_tiles = [&](int k0) {
     at.load(P.a, tid, k0);
-    if constexpr (BKIND == BK_W) bt_w.load(P.w, tid, col0, k0, SPLIT);
+    if constexpr (BKIND == BK_W) bt_w.load(P.w, k0, SPLIT);
     if constexpr (BKIND == BK_ACT) bt_act.load(P.bact, tid, k0);
     if constexpr (BKIND == BK_ACTT) bt_t.load(P.bT, tid, col0, k0);
   };
@@ -293,8 +314,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
   store_tiles(0);
   __syncthreads();
 
-  const int a_off = (wm * TM * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
-  const int b_off = (wn * TN * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
+  const int a_off = lds_off(wm * TM * 16 + (lane & 15), lane >> 4);
+  const int b_off = lds_off(wn * TN * 16 + (lane & 15), lane >> 4);
 
   for (int ks = 0; ks < nk; ++ks) {
     const int cur = ks & 1;
@@ -378,7 +399,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
 // Tiles never straddle a batch (grid.x = B * ceil(T_out / BM)); K order = (chunk, tap).
 constexpr int HALO_MAX = 64;
 
-template <int BM, int BN, int WM, int WN, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool SPLIT, bool PRO>
 __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_per_batch, int T_out) {
   constexpr int TM = BM / (WM * 16);
   constexpr int TN = BN / (WN * 16);
@@ -387,7 +408,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
   constexpr int WCH = WR_MAX * 4;
   constexpr int WPER = (WCH + 255) / 256;
   static_assert(WM * WN == 4, "4 waves");
-  __shared__ __attribute__((aligned(16))) __bf16 Aw[NP][WR_MAX * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) __bf16 Aw[NP][WR_MAX * AW_ROW];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[2][NP][BN * LDS_ROW];
 
   const ActDev& A = P.a;
@@ -398,62 +419,73 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
   const int t0 = (blockIdx.x - b * tiles_per_batch) * BM;
   const int col0 = blockIdx.y * BN;
   const int WR = BM + (A.ksize - 1) * A.dil;
-  const float* xb = A.p + (int64_t)b * A.sb;
   const int nC = A.Cpad / 32;
-  const int steps = nC * A.ksize;
+  const int K = A.ksize;
 
+  // per-thread window rows (fixed across channel chunks): source pointer or null for zero padding
+  const float* wsrc[WPER];
+  int wrow[WPER];
+#pragma unroll
+  for (int i = 0; i < WPER; ++i) {
+    const int c = tid + i * 256;
+    const int w = c >> 2;
+    const int tu = t0 + w - A.pad;
+    int ts = -1;
+    if (c < WCH && w < WR) {
+      if (A.up == 2) ts = (tu >= 0 && tu < 2 * A.T_in) ? (tu >> 1) : -1;
+      else ts = (tu >= 0 && tu < A.T_in) ? tu : -1;
+    }
+    wrow[i] = ts;
+    wsrc[i] = ts >= 0 ? A.p + (int64_t)b * A.sb + (int64_t)ts * A.st + (c & 3) * 8 : nullptr;
+  }
   float wv[WPER][8];
   auto load_window = [&](int cc) {
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
-      const int c = tid + i * 256;
-      const int w = c >> 2, kc = c & 3;
+      if (wsrc[i]) {
+        const float4 x0 = *reinterpret_cast<const float4*>(wsrc[i] + cc * 32);
+        const float4 x1 = *reinterpret_cast<const float4*>(wsrc[i] + cc * 32 + 4);
+        wv[i][0] = x0.x; wv[i][1] = x0.y; wv[i][2] = x0.z; wv[i][3] = x0.w;
+        wv[i][4] = x1.x; wv[i][5] = x1.y; wv[i][6] = x1.z; wv[i][7] = x1.w;
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wv[i][j] = 0.f;
-      if (c >= WCH || w >= WR) continue;
-      const int tu = t0 + w - A.pad;
-      int ts = tu;
-      if (A.up == 2) {
-        if (tu < 0 || tu >= 2 * A.T_in) continue;
-        ts = tu >> 1;
-      } else if (tu < 0 || tu >= A.T_in) {
-        continue;
-      }
-      const int ci = cc * 32 + kc * 8;
-      const float* src = xb + (int64_t)ts * A.st + ci;
-      const float4 x0 = *reinterpret_cast<const float4*>(src);
-      const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-      wv[i][0] = x0.x; wv[i][1] = x0.y; wv[i][2] = x0.z; wv[i][3] = x0.w;
-      wv[i][4] = x1.x; wv[i][5] = x1.y; wv[i][6] = x1.z; wv[i][7] = x1.w;
-      if (A.pm) {
-        const int64_t ri = (int64_t)b * A.T_in + ts;
-        const float mu = A.pm[ri], rs = A.pr[ri];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) wv[i][j] = (wv[i][j] - mu) * rs;
-      }
-      if (A.ps) {
-        const float* sc = A.ps + (int64_t)b * A.psb + ci;
-        const float* sh = A.ph + (int64_t)b * A.psb + ci;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) wv[i][j] = wv[i][j] * sc[j] + sh[j];
-      }
-      if (A.pact) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) wv[i][j] = alcm_act(wv[i][j], A.pact);
+        for (int j = 0; j < 8; ++j) wv[i][j] = 0.f;
       }
     }
   };
-  auto store_window = [&]() {
+  // prologue (normalise / affine / SiLU) is applied at store time so the loads stay in flight
+  // behind the previous chunk's MFMAs; zero-padding rows stay exactly zero
+  auto store_window = [&](int cc) {
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
       const int c = tid + i * 256;
       const int w = c >> 2, kc = c & 3;
       if (c >= WCH || w >= WR) continue;
-      split_store(wv[i], Aw[0] + w * LDS_ROW + kc * 8, Aw[NP - 1] + w * LDS_ROW + kc * 8, SPLIT);
+      if constexpr (PRO) {
+        if (wrow[i] >= 0) {
+          const int ci = cc * 32 + kc * 8;
+          if (A.pm) {
+            const int64_t ri = (int64_t)b * A.T_in + wrow[i];
+            const float mu = A.pm[ri], rs = A.pr[ri];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wv[i][j] = (wv[i][j] - mu) * rs;
+          }
+          if (A.ps) {
+            const float* sc = A.ps + (int64_t)b * A.psb + ci;
+            const float* sh = A.ph + (int64_t)b * A.psb + ci;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wv[i][j] = wv[i][j] * sc[j] + sh[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wv[i][j] = pro_act(wv[i][j], A.pact);
+        }
+      }
+      split_store(wv[i], Aw[0] + w * AW_ROW + kc * 8, Aw[NP - 1] + w * AW_ROW + kc * 8, SPLIT);
     }
   };
 
   WTile<BN> bt;
+  bt.init(P.w, tid, col0);
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -461,58 +493,53 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   load_window(0);
-  bt.load(P.w, tid, col0, 0, SPLIT);
-  store_window();
+  bt.load(P.w, 0, SPLIT);
+  store_window(0);
   bt.template store<SPLIT>(Bs[0][0], Bs[0][NP - 1], tid);
   __syncthreads();
 
-  const int a_base = (wm * TM * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
-  const int b_off = (wn * TN * 16 + (lane & 15)) * LDS_ROW + (lane >> 4) * 8;
-  int cc = 0, tap = 0;
-  for (int s = 0; s < steps; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < steps;
-    if (more) {
-      const int ntap = tap + 1 == A.ksize ? 0 : tap + 1;
-      const int ncc = tap + 1 == A.ksize ? cc + 1 : cc;
-      bt.load(P.w, tid, col0, ntap * A.Cpad + ncc * 32, SPLIT);
-    }
-    const bool new_window = (tap == A.ksize - 1) && (cc + 1 < nC);
-    if (tap == 0 && cc + 1 < nC) load_window(cc + 1);
+  const int a_base = (wm * TM * 16 + (lane & 15)) * AW_ROW + (lane >> 4) * 8;
+  const int b_off = lds_off(wn * TN * 16 + (lane & 15), lane >> 4);
+  int cur = 0;
+  for (int cc = 0; cc < nC; ++cc) {
+    const bool next_win = cc + 1 < nC;
+    if (next_win) load_window(cc + 1);
+    for (int tap = 0; tap < K; ++tap) {
+      const bool last_tap = tap + 1 == K;
+      const bool more = !last_tap || next_win;
+      if (more) bt.load(P.w, last_tap ? (cc + 1) * 32 : (tap + 1) * A.Cpad + cc * 32, SPLIT);
 
-    const int a_off = a_base + tap * A.dil * LDS_ROW;
-    bf16x8 ah[TM], bh[TN];
-    bf16x8 al[SPLIT ? TM : 1], bl[SPLIT ? TN : 1];
+      const int a_off = a_base + tap * A.dil * AW_ROW;
+      bf16x8 ah[TM], bh[TN];
+      bf16x8 al[SPLIT ? TM : 1], bl[SPLIT ? TN : 1];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      ah[i] = *reinterpret_cast<const bf16x8*>(&Aw[0][a_off + i * 16 * LDS_ROW]);
-      if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(&Aw[NP - 1][a_off + i * 16 * LDS_ROW]);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][0][b_off + j * 16 * LDS_ROW]);
-      if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][NP - 1][b_off + j * 16 * LDS_ROW]);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(&Aw[0][a_off + i * 16 * AW_ROW]);
+        if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(&Aw[NP - 1][a_off + i * 16 * AW_ROW]);
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if constexpr (SPLIT) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-        }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][0][b_off + j * 16 * LDS_ROW]);
+        if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][NP - 1][b_off + j * 16 * LDS_ROW]);
       }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
 
-    if (more) bt.template store<SPLIT>(Bs[cur ^ 1][0], Bs[cur ^ 1][NP - 1], tid);
-    if (new_window) {
+      if (more) bt.template store<SPLIT>(Bs[cur ^ 1][0], Bs[cur ^ 1][NP - 1], tid);
+      if (last_tap && next_win) {
+        __syncthreads();
+        store_window(cc + 1);
+      }
       __syncthreads();
-      store_window();
-    }
-    __syncthreads();
-    if (++tap == A.ksize) {
-      tap = 0;
-      ++cc;
+      cur ^= 1;
     }
   }
 
@@ -572,6 +599,10 @@ static bool fill_act(const alcm_operand& o, int M, ActDev& d, std::string& err) 
     err = "bad ACT operand geometry";
     return false;
   }
+  if (o.pro_act != ACT_NONE && o.pro_act != ACT_SILU) {
+    err = "prologue activation must be NONE or SILU";
+    return false;
+  }
   if ((o.pro_scale == nullptr) != (o.pro_shift == nullptr) || (o.pro_mean == nullptr) != (o.pro_rstd == nullptr)) {
     err = "prologue scale/shift and mean/rstd must come in pairs";
     return false;
@@ -610,18 +641,24 @@ static void launch_split(const GemmDev& P, int batch, int ncols, bool split, hip
   else launch_one<BM, BN, WM, WN, AVEC, BKIND, false>(P, batch, ncols, s);
 }
 
-template <int BM, int BN, int WM, int WN, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool SPLIT, bool PRO>
 static void launch_conv(const GemmDev& P, int nbatch, int T_out, hipStream_t s) {
   const int tpb = (T_out + BM - 1) / BM;
   dim3 grid(nbatch * tpb, (P.N + BN - 1) / BN, 1);
   void* tok = prof_start(s);
-  hipLaunchKernelGGL((conv_kernel<BM, BN, WM, WN, SPLIT>), grid, dim3(256), 0, s, P, tpb, T_out);
+  hipLaunchKernelGGL((conv_kernel<BM, BN, WM, WN, SPLIT, PRO>), grid, dim3(256), 0, s, P, tpb, T_out);
   if (tok) {
     char name[128];
-    std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %s>", BM, BN, WM, WN,
-                  SPLIT ? "true" : "false");
+    std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %s, %s>", BM, BN, WM, WN,
+                  SPLIT ? "true" : "false", PRO ? "true" : "false");
     prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
   }
+}
+
+template <int BM, int BN, int WM, int WN, bool PRO>
+static void launch_conv_sp(const GemmDev& P, int nbatch, int T_out, bool split, hipStream_t s) {
+  if (split) launch_conv<BM, BN, WM, WN, true, PRO>(P, nbatch, T_out, s);
+  else launch_conv<BM, BN, WM, WN, false, PRO>(P, nbatch, T_out, s);
 }
 
 int gemm(const alcm_gemm_args& g, hipStream_t s) {
@@ -691,12 +728,13 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
     const int nb = g.M / g.a.rows_per_batch, T_out = g.a.rows_per_batch;
     // 64-wide N tiles when 128-wide tiles would waste a third of the MFMA work (N = 192, 320, ...)
     const bool narrow = g.tile_n == 64 || (g.tile_n == 0 && (N <= 64 || (N % 128 != 0 && N % 64 == 0)));
+    const bool pro = g.a.pro_scale || g.a.pro_mean || g.a.pro_act;
     if (narrow) {
-      if (split) launch_conv<128, 64, 4, 1, true>(P, nb, T_out, s);
-      else launch_conv<128, 64, 4, 1, false>(P, nb, T_out, s);
+      if (pro) launch_conv_sp<128, 64, 4, 1, true>(P, nb, T_out, split, s);
+      else launch_conv_sp<128, 64, 4, 1, false>(P, nb, T_out, split, s);
     } else {
-      if (split) launch_conv<128, 128, 2, 2, true>(P, nb, T_out, s);
-      else launch_conv<128, 128, 2, 2, false>(P, nb, T_out, s);
+      if (pro) launch_conv_sp<128, 128, 2, 2, true>(P, nb, T_out, split, s);
+      else launch_conv_sp<128, 128, 2, 2, false>(P, nb, T_out, split, s);
     }
   } else if (bkind == BK_W) {
     if (N <= 32) {

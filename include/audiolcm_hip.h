@@ -71,7 +71,8 @@ typedef struct alcm_operand {
   int rows;           /* ACT_T / WEIGHT: number of valid rows */
   int64_t zs1, zs2;   /* batched offset (z / zdiv)*zs1 + (z % zdiv)*zs2 */
   /* ACT prologue, applied to valid (non-padding) elements: v = (v - mean[b*T_in+t_src]) * rstd[...]
-   * (if pro_mean), v = v*pro_scale[b*pro_sb+c] + pro_shift[...] (if pro_scale), v = act(v) */
+   * (if pro_mean), v = v*pro_scale[b*pro_sb+c] + pro_shift[...] (if pro_scale), v = act(v)
+   * with pro_act 0 (none) or 1 (SiLU); other codes are rejected with ALCM_E_INVALID */
   const float* pro_scale;
   const float* pro_shift;
   int64_t pro_sb;
@@ -85,7 +86,8 @@ typedef struct alcm_gemm_args {
   int M, N, Kpad; /* Kpad: multiple of 32 covering the real K */
   int batch, zdiv;
   alcm_operand a, b;
-  /* epilogue: v = acc*acc_scale + bias[n]; v = act(v) (geglu: v_even * gelu_erf(v_odd) -> column n/2);
+  /* activation codes: 0 none, 1 SiLU, 2 GELU (erf), 3 GELU (tanh), 4 tanh
+   * epilogue: v = acc*acc_scale + bias[n]; v = act(v) (geglu: v_even * gelu_erf(v_odd) -> column n/2);
    *           v += res[...]; v *= out_scale; if accumulate v += out[...]; out[...] = v
    * output row m -> (b, t), stored at out + zoff + b*o_sb + (t*out_step + out_off)*o_st + n*o_sc */
   const float* bias;

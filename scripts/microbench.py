@@ -76,8 +76,30 @@ def bench_act(B=32):
         print(f"act1d C={C} T={T}: {ms:.3f} ms {B * T * C * 8 / 1e9 / ms:.2f} TB/s")
 
 
+def bench_amp_one(B=32, C=24, k=3, d=1, reps=5):
+    """single configuration (target for rocprofv3 --pmc passes)"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    T = 3833856 // C
+    x = torch.randn((B, T, C), device="cuda")
+    r = torch.randn((B, T, C), device="cuda")
+    a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+    w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+    ms = timeit(lambda: K.amp_conv(x, w, None, d, (k * d - d) // 2, act=(a, bt, f, f), residual=r), reps=reps)
+    print(f"amp1 C={C} k={k} d={d}: {ms:.3f} ms {B * T * C * 12 / 1e9 / ms:.2f} TB/s")
+
+
+def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
+    """single window-conv configuration (target for rocprofv3 --pmc passes)"""
+    x = torch.randn((B, T, C), device="cuda")
+    w = torch.randn((C, C, k), device="cuda") * (1 / (C * k) ** 0.5)
+    pw = K.pack_conv_weight(w)
+    ms = timeit(lambda: K.conv1d(x, w, None, padding=(k * d - d) // 2, dilation=d, split=split, channels_last=True,
+                                 packed=pw), reps=3)
+    print(f"conv1 C={C} k={k}: {ms:.3f} ms {2 * B * T * C * C * k / 1e9 / ms:.1f} TF/s algorithmic")
+
+
 if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["amp", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "conv": bench_conv, "act": bench_act}[w]()
+        {"amp": bench_amp, "conv": bench_conv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
