@@ -66,6 +66,17 @@ def cpu_baseline(clips: int, latent_len: int, lcm_steps: int):
                        f"fp32 torch-CPU oracle, {dt:.1f} s wall")
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC pass (profiles/<tag>/kernels.json,
+    written by scripts/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE runs of this bench)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*", "kernels.json")), reverse=True):
+        rec = json.load(open(path)).get(kernel)
+        if rec and rec.get("hbm_bytes_per_launch"):
+            return dict(bytes_per_launch=round(rec["hbm_bytes_per_launch"]), source=os.path.relpath(path, HERE))
+    return None
+
+
 def main():
     a = parse()
     from audiolcm_amd import _hip, recipe
@@ -125,7 +136,7 @@ def main():
         else:
             ach, peak, unit = dom["bytes"] / sec / 1e9, _hip.PEAK_HBM_BYTES / 1e9, "GB/s"
         roofline = dict(bound="mfma" if mfma else "hbm", achieved=round(ach, 2), peak=peak, unit=unit,
-                        frac=round(ach / peak, 4), traffic=None, kernel=dom["name"], launches=dom["launches"],
+                        frac=round(ach / peak, 4), traffic=pmc_traffic(dom["name"]), kernel=dom["name"], launches=dom["launches"],
                         avg_launch_us=round(1e3 * dom["total_ms"] / dom["launches"], 2),
                         per_launch_algorithmic=round((dom["flops"] if mfma else dom["bytes"]) / dom["launches"], 1),
                         kernel_share_of_gpu_time=round(dom["total_ms"] / max(gpu_ms, 1e-9), 4),
