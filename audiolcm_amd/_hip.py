@@ -17,6 +17,9 @@ LIB_PATH = os.environ.get("ALCM_LIB", os.path.join(HERE, "libaudiolcm_hip.so"))
 ALCM_OPND_ACT, ALCM_OPND_ACT_T, ALCM_OPND_WEIGHT = 0, 1, 2
 ALCM_MODEL_DIT, ALCM_MODEL_VAE, ALCM_MODEL_BIGVGAN = 0, 1, 2
 ACT_NONE, ACT_SILU, ACT_GELU_ERF, ACT_GELU_TANH, ACT_TANH = 0, 1, 2, 3, 4
+PREC_BF16, PREC_SPLIT, PREC_F16 = 0, 1, 2              # per-launch MFMA operand precision
+POLICY_BF16, POLICY_SPLIT, POLICY_MIXED = 0, 1, 2      # per-model precision policy
+POLICIES = {"bf16": POLICY_BF16, "split": POLICY_SPLIT, "mixed": POLICY_MIXED}
 
 i64 = C.c_int64
 vp = C.c_void_p
@@ -37,7 +40,7 @@ class GemmArgs(C.Structure):
                 ("act", C.c_int), ("accumulate", C.c_int), ("geglu", C.c_int), ("res", fp),
                 ("r_sb", i64), ("r_st", i64), ("r_sc", i64), ("r_zs1", i64), ("r_zs2", i64), ("out", fp),
                 ("o_sb", i64), ("o_st", i64), ("o_sc", i64), ("o_zs1", i64), ("o_zs2", i64),
-                ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("split", C.c_int),
+                ("out_rows_per_batch", C.c_int), ("out_step", C.c_int), ("out_off", C.c_int), ("prec", C.c_int),
                 ("disable_window", C.c_int), ("tile_n", C.c_int)]
 
 
@@ -46,7 +49,7 @@ class AmpArgs(C.Structure):
                 ("alpha_exp", fp), ("inv_beta", fp), ("up_filter", fp), ("down_filter", fp), ("w", vp),
                 ("w_lo_off", i64), ("kpad", C.c_int), ("Cout", C.c_int), ("ksize", C.c_int), ("dil", C.c_int),
                 ("pad", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
-                ("accumulate", C.c_int), ("out_scale", C.c_float), ("split", C.c_int)]
+                ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int)]
 
 
 class NamedTensor(C.Structure):
@@ -81,6 +84,7 @@ _SIGS = [
     ("alcm_model_destroy", C.c_int, [vp]),
     ("alcm_model_weight_bytes", C.c_size_t, [vp]),
     ("alcm_model_set_split", C.c_int, [vp, C.c_int]),
+    ("alcm_model_set_precision", C.c_int, [vp, C.c_int]),
     ("alcm_dit_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_dit_embed_context", C.c_int, [vp, fp, C.c_int, fp, vp, C.c_size_t, vp]),
     ("alcm_dit_forward", C.c_int, [vp, fp, vp, fp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),

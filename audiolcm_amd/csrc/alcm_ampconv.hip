@@ -119,7 +119,7 @@ __device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st
 
 // BM output rows per workgroup (4 waves x BM/4 rows), all Cout (<= TN*16) columns.
 constexpr int AMP_WAVES = 8;  // 512-thread workgroups: one activation item per thread, more waves in flight
-template <int BM, int TN, int CPAD, bool SPLIT, bool ACT>
+template <int BM, int TN, int CPAD, int PREC, bool ACT>
 __global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P) {
   constexpr int NT = 64 * AMP_WAVES;
   constexpr int WROWS = BM / AMP_WAVES;  // output rows per wave
@@ -127,6 +127,7 @@ __global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P
   static_assert(TM >= 1 && WROWS % 16 == 0, "BM must give each wave a multiple of 16 rows");
   constexpr int S = CPAD + 8 + ((8 - (CPAD + 8) % 32 + 32) % 32);  // row stride (bf16) == 8 mod 32
   constexpr int WR_MAX = BM + 64;
+  constexpr bool SPLIT = PREC == PREC_SPLIT;
   constexpr int NP = SPLIT ? 2 : 1;
   __shared__ __attribute__((aligned(16))) __bf16 Wn[NP][WR_MAX * S];
 
@@ -163,9 +164,13 @@ __global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P
 #pragma unroll
     for (int r = 0; r < AR; ++r) {
       const int w = run * AR + r;
-      const __bf16 h = (__bf16)o[r];
-      Wn[0][w * S + c] = h;
-      if (SPLIT) Wn[NP - 1][w * S + c] = (__bf16)(o[r] - (float)h);
+      if constexpr (PREC == PREC_F16) {
+        Wn[0][w * S + c] = __builtin_bit_cast(__bf16, (_Float16)o[r]);
+      } else {
+        const __bf16 h = (__bf16)o[r];
+        Wn[0][w * S + c] = h;
+        if (SPLIT) Wn[NP - 1][w * S + c] = (__bf16)(o[r] - (float)h);
+      }
     }
   }
   __syncthreads();
@@ -231,10 +236,10 @@ __global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (SPLIT) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<PREC>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC>(ah[i], bl[j], acc[i][j]);
         }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
       }
   }
 
@@ -262,23 +267,26 @@ __global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P
   }
 }
 
+template <int BM, int TN, int CPAD, int PREC>
+static void launch_amp_p(const AmpDev& Q, dim3 grid, bool act, hipStream_t s) {
+  if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, PREC, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
+  else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, PREC, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
+}
+
 template <int BM, int TN, int CPAD>
-static void launch_amp(const AmpDev& P, int B, bool split, bool act, hipStream_t s) {
+static void launch_amp(const AmpDev& P, int B, int prec, bool act, hipStream_t s) {
   AmpDev Q = P;
   Q.tiles_per_batch = (P.T + BM - 1) / BM;
   dim3 grid(B * Q.tiles_per_batch);
   void* tok = prof_start(s);
-  if (split) {
-    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
-    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, true, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
-  } else {
-    if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
-    else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, false, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
-  }
+  if (prec == PREC_SPLIT) launch_amp_p<BM, TN, CPAD, PREC_SPLIT>(Q, grid, act, s);
+  else if (prec == PREC_F16) launch_amp_p<BM, TN, CPAD, PREC_F16>(Q, grid, act, s);
+  else launch_amp_p<BM, TN, CPAD, PREC_BF16>(Q, grid, act, s);
+  const bool split = prec == PREC_SPLIT;
   if (tok) {
     char name[128];
-    std::snprintf(name, sizeof(name), "alcm::amp_conv_kernel<%d, %d, %d, %s, %s>", BM, TN, CPAD,
-                  split ? "true" : "false", act ? "true" : "false");
+    std::snprintf(name, sizeof(name), "alcm::amp_conv_kernel<%d, %d, %d, %d, %s>", BM, TN, CPAD, prec,
+                  act ? "true" : "false");
     const double elems = (double)B * P.T;
     const double flops = 2.0 * elems * P.Cout * (double)P.ksize * P.Cin;
     const double bytes = elems * (P.Cin + P.Cout * (1 + (P.res ? 1 : 0) + (P.accumulate ? 1 : 0))) * 4.0 +
@@ -304,11 +312,14 @@ int amp_conv(const alcm_amp_args& a, hipStream_t s) {
       P.f.up[k] = a.up_filter[k];
       P.f.dn[k] = a.down_filter[k];
     }
-  P.w = (const u16*)a.w; P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.Cout = a.Cout; P.ksize = a.ksize;
+  if (a.prec < PREC_BF16 || a.prec > PREC_F16) return set_error(ALCM_E_INVALID, "amp_conv: bad prec");
+  // PREC_F16 reads the packed weight's fp16 plane (ptr + 2*w_lo_off)
+  P.w = (const u16*)a.w + (a.prec == PREC_F16 ? 2 * a.w_lo_off : 0); P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.Cout = a.Cout; P.ksize = a.ksize;
   P.dil = a.dil; P.pad = a.pad; P.bias = a.bias; P.res = a.res; P.r_sb = (int64_t)a.T * a.Cout;
   P.out = a.out; P.o_sb = (int64_t)a.T * a.Cout; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
-  const bool split = a.split != 0, act = a.act != 0;
+  const int split = a.prec;
+  const bool act = a.act != 0;
   if (cpad != a.Cin) return set_error(ALCM_E_INVALID, "amp_conv: Cin must be a multiple of 8");
   if (a.Cin == 24 && a.Cout <= 16) launch_amp<256, 1, 24>(P, a.B, split, act, s);
   else if (a.Cin == 24 && a.Cout <= 32) launch_amp<256, 2, 24>(P, a.B, split, act, s);

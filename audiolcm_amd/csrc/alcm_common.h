@@ -6,6 +6,7 @@
 #define ALCM_WAVE 64
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
@@ -27,6 +28,22 @@ struct FastDiv {
     r = n - q * d;
   }
 };
+
+// MFMA operand precision (alcm_gemm_args.prec / alcm_amp_args.prec):
+//   PREC_BF16  one bf16 MFMA (operands rounded to bf16)
+//   PREC_SPLIT bf16x3: hi*hi + hi*lo + lo*hi, ~fp32 accuracy
+//   PREC_F16   one fp16 MFMA (operands rounded to fp16, 8x finer than bf16)
+enum AlcmPrec : int { PREC_BF16 = 0, PREC_SPLIT = 1, PREC_F16 = 2 };
+
+// 16x16x32 MFMA step on 16-byte operand fragments held as bf16x8 (fp16 bits for PREC_F16).
+template <int PREC>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (PREC == PREC_F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 // Activation codes shared by GEMM prologue/epilogue and elementwise kernels.
 enum AlcmAct : int {

@@ -12,7 +12,9 @@
 // they are staged into LDS and fed to v_mfma_f32_16x16x32_bf16 with fp32 accumulate.  With
 // SPLIT each fp32 operand is carried as hi = bf16(x), lo = bf16(x - hi) and the product is
 // hi*hi + hi*lo + lo*hi (3 MFMAs): ~2^-16 relative error, i.e. fp32-reference parity at 3x
-// the bf16 MFMA cost (still 5.3x the f32-input MFMA rate).
+// the bf16 MFMA cost (still 5.3x the f32-input MFMA rate).  PREC_F16 rounds both operands to fp16
+// (11-bit significand, 8x smaller rounding error than bf16) and runs v_mfma_f32_16x16x32_f16 once:
+// the per-layer precision policy (alcm_models.cpp) uses it where the parity budget allows.
 //
 // Prologue (A operand, applied on load): GroupNorm/LayerNorm affine + SiLU, so norm+act+conv
 // is one pass over HBM.  Epilogue: bias, acc scale, activation, GEGLU pair gating
@@ -94,16 +96,25 @@ __device__ __forceinline__ int64_t zoff(const FastDiv& zd, int z, int64_t s1, in
   return (int64_t)q * s1 + (int64_t)r * s2;
 }
 
-__device__ __forceinline__ void split_store(const float (&v)[8], __bf16* hi, __bf16* lo, bool split) {
-  bf16x8 h, l;
+// fp32 -> MFMA operand planes: bf16 hi (+ bf16 lo for PREC_SPLIT) or fp16 (PREC_F16, in the hi plane)
+template <int PREC>
+__device__ __forceinline__ void prec_store(const float (&v)[8], __bf16* hi, __bf16* lo) {
+  if constexpr (PREC == PREC_F16) {
+    f16x8 h;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 bh = (__bf16)v[j];
-    h[j] = bh;
-    if (split) l[j] = (__bf16)(v[j] - (float)bh);
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
+    *reinterpret_cast<f16x8*>(hi) = h;
+  } else {
+    bf16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 bh = (__bf16)v[j];
+      h[j] = bh;
+      if (PREC == PREC_SPLIT) l[j] = (__bf16)(v[j] - (float)bh);
+    }
+    *reinterpret_cast<bf16x8*>(hi) = h;
+    if (PREC == PREC_SPLIT) *reinterpret_cast<bf16x8*>(lo) = l;
   }
-  *reinterpret_cast<bf16x8*>(hi) = h;
-  if (split) *reinterpret_cast<bf16x8*>(lo) = l;
 }
 
 // ---------------------------------------------------------------- fp32 activation tile (conv taps)
@@ -178,14 +189,14 @@ struct ActTile {
       }
     }
   }
-  template <bool SPLIT>
+  template <int PREC>
   __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       if (c >= CHUNKS) continue;
       const int off = lds_off(c >> 2, c & 3);
-      split_store(v[i], hi + off, lo + off, SPLIT);
+      prec_store<PREC>(v[i], hi + off, lo + off);
     }
   }
 };
@@ -211,14 +222,14 @@ struct ActTTile {
       }
     }
   }
-  template <bool SPLIT>
+  template <int PREC>
   __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 256;
       if (c >= CHUNKS) continue;
       const int off = lds_off(c % ROWS, c / ROWS);
-      split_store(v[i], hi + off, lo + off, SPLIT);
+      prec_store<PREC>(v[i], hi + off, lo + off);
     }
   }
 };
@@ -251,7 +262,7 @@ struct WTile {
       }
     }
   }
-  template <bool SPLIT>
+  template <int PREC>
   __device__ __forceinline__ void store(__bf16* hi, __bf16* lo, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -259,16 +270,17 @@ struct WTile {
       if (c >= CHUNKS) continue;
       const int off = lds_off(c >> 2, c & 3);
       *reinterpret_cast<uint4*>(hi + off) = h[i];
-      if (SPLIT) *reinterpret_cast<uint4*>(lo + off) = l[i];
+      if (PREC == PREC_SPLIT) *reinterpret_cast<uint4*>(lo + off) = l[i];
     }
   }
 };
 
 // ---------------------------------------------------------------- the kernel
-template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, int PREC>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
   constexpr int TM = BM / (WM * 16);
   constexpr int TN = BN / (WN * 16);
+  constexpr bool SPLIT = PREC == PREC_SPLIT;
   constexpr int NP = SPLIT ? 2 : 1;
   static_assert(WM * WN == 4, "4 waves");
   __shared__ __attribute__((aligned(16))) __bf16 As[2][NP][BM * LDS_ROW];
@@ -297,10 +309,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
     if constexpr (BKIND == BK_ACTT) bt_t.load(P.bT, tid, col0, k0);
   };
   auto store_tiles = [&](int buf) {
-    at.template store<SPLIT>(As[buf][0], As[buf][NP - 1], tid);
-    if constexpr (BKIND == BK_W) bt_w.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
-    if constexpr (BKIND == BK_ACT) bt_act.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
-    if constexpr (BKIND == BK_ACTT) bt_t.template store<SPLIT>(Bs[buf][0], Bs[buf][NP - 1], tid);
+    at.template store<PREC>(As[buf][0], As[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_W) bt_w.template store<PREC>(Bs[buf][0], Bs[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_ACT) bt_act.template store<PREC>(Bs[buf][0], Bs[buf][NP - 1], tid);
+    if constexpr (BKIND == BK_ACTT) bt_t.template store<PREC>(Bs[buf][0], Bs[buf][NP - 1], tid);
   };
 
   f32x4 acc[TM][TN];
@@ -338,10 +350,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (SPLIT) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<PREC>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC>(ah[i], bl[j], acc[i][j]);
         }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
       }
 
     if (ks + 1 < nk) store_tiles(cur ^ 1);
@@ -399,10 +411,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
 // Tiles never straddle a batch (grid.x = B * ceil(T_out / BM)); K order = (chunk, tap).
 constexpr int HALO_MAX = 64;
 
-template <int BM, int BN, int WM, int WN, bool SPLIT, bool PRO>
+template <int BM, int BN, int WM, int WN, int PREC, bool PRO>
 __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_per_batch, int T_out) {
   constexpr int TM = BM / (WM * 16);
   constexpr int TN = BN / (WN * 16);
+  constexpr bool SPLIT = PREC == PREC_SPLIT;
   constexpr int NP = SPLIT ? 2 : 1;
   constexpr int WR_MAX = BM + HALO_MAX;
   constexpr int WCH = WR_MAX * 4;
@@ -480,7 +493,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
           for (int j = 0; j < 8; ++j) wv[i][j] = pro_act(wv[i][j], A.pact);
         }
       }
-      split_store(wv[i], Aw[0] + w * AW_ROW + kc * 8, Aw[NP - 1] + w * AW_ROW + kc * 8, SPLIT);
+      prec_store<PREC>(wv[i], Aw[0] + w * AW_ROW + kc * 8, Aw[NP - 1] + w * AW_ROW + kc * 8);
     }
   };
 
@@ -495,7 +508,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
   load_window(0);
   bt.load(P.w, 0, SPLIT);
   store_window(0);
-  bt.template store<SPLIT>(Bs[0][0], Bs[0][NP - 1], tid);
+  bt.template store<PREC>(Bs[0][0], Bs[0][NP - 1], tid);
   __syncthreads();
 
   const int a_base = (wm * TM * 16 + (lane & 15)) * AW_ROW + (lane >> 4) * 8;
@@ -527,13 +540,13 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (SPLIT) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16<PREC>(al[i], bh[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC>(ah[i], bl[j], acc[i][j]);
           }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
         }
 
-      if (more) bt.template store<SPLIT>(Bs[cur ^ 1][0], Bs[cur ^ 1][NP - 1], tid);
+      if (more) bt.template store<PREC>(Bs[cur ^ 1][0], Bs[cur ^ 1][NP - 1], tid);
       if (last_tap && next_win) {
         __syncthreads();
         store_window(cc + 1);
@@ -621,44 +634,46 @@ struct LaunchCost {
 };
 static thread_local LaunchCost g_cost;
 
-template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND, int PREC>
 static void launch_one(const GemmDev& P, int batch, int ncols, hipStream_t s) {
   dim3 grid((P.M + BM - 1) / BM, (ncols + BN - 1) / BN, batch);
   void* tok = prof_start(s);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AVEC, BKIND, SPLIT>), grid, dim3(256), 0, s, P);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AVEC, BKIND, PREC>), grid, dim3(256), 0, s, P);
   if (tok) {
     // the demangled name rocprofv3 prints for this instantiation
     char name[128];
-    std::snprintf(name, sizeof(name), "alcm::gemm_kernel<%d, %d, %d, %d, %s, %d, %s>", BM, BN, WM, WN,
-                  AVEC ? "true" : "false", BKIND, SPLIT ? "true" : "false");
+    std::snprintf(name, sizeof(name), "alcm::gemm_kernel<%d, %d, %d, %d, %s, %d, %d>", BM, BN, WM, WN,
+                  AVEC ? "true" : "false", BKIND, PREC);
     prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
   }
 }
 
 template <int BM, int BN, int WM, int WN, bool AVEC, int BKIND>
-static void launch_split(const GemmDev& P, int batch, int ncols, bool split, hipStream_t s) {
-  if (split) launch_one<BM, BN, WM, WN, AVEC, BKIND, true>(P, batch, ncols, s);
-  else launch_one<BM, BN, WM, WN, AVEC, BKIND, false>(P, batch, ncols, s);
+static void launch_split(const GemmDev& P, int batch, int ncols, int prec, hipStream_t s) {
+  if (prec == PREC_SPLIT) launch_one<BM, BN, WM, WN, AVEC, BKIND, PREC_SPLIT>(P, batch, ncols, s);
+  else if (prec == PREC_F16) launch_one<BM, BN, WM, WN, AVEC, BKIND, PREC_F16>(P, batch, ncols, s);
+  else launch_one<BM, BN, WM, WN, AVEC, BKIND, PREC_BF16>(P, batch, ncols, s);
 }
 
-template <int BM, int BN, int WM, int WN, bool SPLIT, bool PRO>
+template <int BM, int BN, int WM, int WN, int PREC, bool PRO>
 static void launch_conv(const GemmDev& P, int nbatch, int T_out, hipStream_t s) {
   const int tpb = (T_out + BM - 1) / BM;
   dim3 grid(nbatch * tpb, (P.N + BN - 1) / BN, 1);
   void* tok = prof_start(s);
-  hipLaunchKernelGGL((conv_kernel<BM, BN, WM, WN, SPLIT, PRO>), grid, dim3(256), 0, s, P, tpb, T_out);
+  hipLaunchKernelGGL((conv_kernel<BM, BN, WM, WN, PREC, PRO>), grid, dim3(256), 0, s, P, tpb, T_out);
   if (tok) {
     char name[128];
-    std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %s, %s>", BM, BN, WM, WN,
-                  SPLIT ? "true" : "false", PRO ? "true" : "false");
+    std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %d, %s>", BM, BN, WM, WN, PREC,
+                  PRO ? "true" : "false");
     prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
   }
 }
 
 template <int BM, int BN, int WM, int WN, bool PRO>
-static void launch_conv_sp(const GemmDev& P, int nbatch, int T_out, bool split, hipStream_t s) {
-  if (split) launch_conv<BM, BN, WM, WN, true, PRO>(P, nbatch, T_out, s);
-  else launch_conv<BM, BN, WM, WN, false, PRO>(P, nbatch, T_out, s);
+static void launch_conv_sp(const GemmDev& P, int nbatch, int T_out, int prec, hipStream_t s) {
+  if (prec == PREC_SPLIT) launch_conv<BM, BN, WM, WN, PREC_SPLIT, PRO>(P, nbatch, T_out, s);
+  else if (prec == PREC_F16) launch_conv<BM, BN, WM, WN, PREC_F16, PRO>(P, nbatch, T_out, s);
+  else launch_conv<BM, BN, WM, WN, PREC_BF16, PRO>(P, nbatch, T_out, s);
 }
 
 int gemm(const alcm_gemm_args& g, hipStream_t s) {
@@ -677,7 +692,9 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
   int bkind;
   if (g.b.kind == ALCM_OPND_WEIGHT) {
     bkind = BK_W;
-    P.w.p = (const u16*)g.b.ptr; P.w.lo = g.b.w_lo_off; P.w.rows = g.b.rows; P.w.Kpad = g.Kpad;
+    // PREC_F16 reads the fp16 plane (third plane of the packed weight) in place of bf16 hi
+    P.w.p = (const u16*)g.b.ptr + (g.prec == PREC_F16 ? 2 * g.b.w_lo_off : 0);
+    P.w.lo = g.b.w_lo_off; P.w.rows = g.b.rows; P.w.Kpad = g.Kpad;
     if (!g.b.ptr || g.b.rows < g.N) return set_error(ALCM_E_INVALID, "weight operand rows < N");
     if ((((uintptr_t)g.b.ptr) & 15) || (g.b.w_lo_off % 8)) return set_error(ALCM_E_INVALID, "weight alignment");
   } else if (g.b.kind == ALCM_OPND_ACT) {
@@ -704,7 +721,8 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
   E.out_off = g.out_off;
 
   const bool avec = act_vec_ok(g.a);
-  const bool split = g.split != 0;
+  if (g.prec < PREC_BF16 || g.prec > PREC_F16) return set_error(ALCM_E_INVALID, "prec must be 0 (bf16), 1 (split) or 2 (f16)");
+  const int split = g.prec;  // precision code passed down to the launchers
   const int N = g.N;
   if (prof_enabled()) {
     // algorithmic work of this launch: 2*M*N*K_real MACs; unique A rows, B operand, output (+residual/acc)
@@ -712,7 +730,7 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
     const double nb = (double)batch;
     const double a_rows = (double)g.a.T_in * ((double)g.M / std::max(1, g.a.rows_per_batch));
     double bbytes;
-    if (bkind == BK_W) bbytes = (double)N * g.Kpad * 2.0 * (split ? 2 : 1);
+    if (bkind == BK_W) bbytes = (double)N * g.Kpad * 2.0 * (split == PREC_SPLIT ? 2 : 1);
     else if (bkind == BK_ACT) bbytes = nb * (double)g.b.T_in * g.b.C_in * 4.0;
     else bbytes = nb * (double)g.b.rows * g.b.T_in * 4.0;
     const double nout = g.geglu ? N / 2 : N;
@@ -763,7 +781,7 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- weight packing (device)
-// W[co][ci][k] fp32 -> bf16 hi/lo [co][Kpad], K index = tap*cpad + ci.  For ConvTranspose1d
+// W[co][ci][k] fp32 -> planes bf16 hi, bf16 lo, fp16 [co][Kpad], K index = tap*cpad + ci.  For ConvTranspose1d
 // (weight [ci][co][k], stride s, phase r) tap j = r + s*(Q-1-tap).
 __global__ void pack_weight_kernel(const float* w, int c_out, int c_in, int ksz, int cpad, int kpad, int transposed,
                                    int stride, int phase, u16* out) {
@@ -786,6 +804,7 @@ __global__ void pack_weight_kernel(const float* w, int c_out, int c_in, int ksz,
     const __bf16 l = (__bf16)(v - (float)h);
     out[idx] = __builtin_bit_cast(u16, h);
     out[idx + total] = __builtin_bit_cast(u16, l);
+    out[idx + 2 * total] = __builtin_bit_cast(u16, (_Float16)v);
   }
 }
 

@@ -102,7 +102,7 @@ struct VocW {
 
 struct alcm_model {
   int kind = -1;
-  int split = 1;
+  int policy = ALCM_POLICY_SPLIT;  // ALCM_POLICY_*
   std::vector<void*> allocs;
   size_t weight_bytes = 0;
   alcm::DitW dit;
@@ -111,6 +111,13 @@ struct alcm_model {
 };
 
 namespace alcm {
+
+// MFMA precision of one layer under the model's policy; f16_ok marks the layers the parity budget lets
+// run as one fp16 MFMA (measured by scripts/precision_emulate.py).
+static int prec_of(const alcm_model* m, bool f16_ok) {
+  if (m->policy == ALCM_POLICY_BF16) return PREC_BF16;
+  return (m->policy == ALCM_POLICY_MIXED && f16_ok) ? PREC_F16 : PREC_SPLIT;
+}
 
 struct Error : std::runtime_error {
   int code;
@@ -160,7 +167,7 @@ struct Ingest {
       throw Error(ALCM_E_HIP, "hipMemcpy H2D failed");
     return p;
   }
-  // pack W[co][ci][k] (or ConvTranspose [ci][co][k] phase) into bf16 hi/lo [rows][kpad]
+  // pack W[co][ci][k] (or ConvTranspose [ci][co][k] phase) into bf16 hi / bf16 lo / fp16 [rows][kpad]
   Packed pack(const std::vector<float>& w, int cout, int cin, int k, int transposed = 0, int stride = 1,
               int phase = 0) {
     Packed P;
@@ -170,7 +177,7 @@ struct Ingest {
     P.taps = transposed ? k / stride : k;
     P.kpad = round_up(P.taps * P.cpad, kBK);
     P.lo = (int64_t)cout * P.kpad;
-    P.p = (u16*)dalloc((size_t)2 * cout * P.kpad * sizeof(u16));
+    P.p = (u16*)dalloc((size_t)3 * cout * P.kpad * sizeof(u16));  // bf16 hi, bf16 lo, fp16 planes
     void* tmp = nullptr;
     if (hipMalloc(&tmp, w.size() * sizeof(float)) != hipSuccess) throw Error(ALCM_E_HIP, "hipMalloc tmp failed");
     (void)hipMemcpy(tmp, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -512,7 +519,7 @@ static int conv(hipStream_t s, int split, int B, int rows_per_batch, const View&
   g.out_rows_per_batch = rows_per_batch;
   g.out_step = o.step;
   g.out_off = o.off;
-  g.split = split;
+  g.prec = split;
   return gemm(g, s);
 }
 
@@ -568,7 +575,7 @@ static int dit_attention(hipStream_t s, int split, const DitW& D, int B, int L, 
   g.out_scale = 1.f;
   g.out = S; g.o_sb = 0; g.o_st = Lp; g.o_sc = 1; g.o_zs1 = (int64_t)nh * L * Lp; g.o_zs2 = (int64_t)L * Lp;
   g.out_rows_per_batch = L; g.out_step = 1;
-  g.split = split;
+  g.prec = split;
   ALCM_TRY(gemm(g, s));
   ALCM_TRY(softmax_rows(S, B * nh * L, L, Lp, s));
   // O = P V
@@ -583,7 +590,7 @@ static int dit_attention(hipStream_t s, int split, const DitW& D, int B, int L, 
   p.acc_scale = 1.f; p.out_scale = 1.f;
   p.out = O; p.o_sb = 0; p.o_st = H; p.o_sc = 1; p.o_zs1 = (int64_t)L * H; p.o_zs2 = dh;
   p.out_rows_per_batch = L; p.out_step = 1;
-  p.split = split;
+  p.prec = split;
   return gemm(p, s);
 }
 
@@ -600,8 +607,8 @@ static int dit_embed_context(alcm_model* m, const float* ctx, int B, float* cemb
     View x{ctx + (int64_t)e * n * D.ctx_dim, (int64_t)CT * D.ctx_dim, D.ctx_dim, 1, n, D.ctx_dim};
     ConvOpts o1;
     o1.act = ACT_GELU_TANH;
-    ALCM_TRY(conv(s, m->split, B, n, x, D.c0[e], ocl(t0, n, H), o1));
-    ALCM_TRY(conv(s, m->split, B, n, cl(t0, n, H), D.c2[e], ocl(t1, n, H), ConvOpts{}));
+    ALCM_TRY(conv(s, prec_of(m, false), B, n, x, D.c0[e], ocl(t0, n, H), o1));
+    ALCM_TRY(conv(s, prec_of(m, false), B, n, cl(t0, n, H), D.c2[e], ocl(t1, n, H), ConvOpts{}));
     // LayerNorm, plus the learned position rows 1+e*n .. (PositionEmbedding MODE_ADD, new_attention.py:245-248)
     for (int b = 0; b < B; ++b)
       ALCM_TRY(layer_norm(t1 + (int64_t)b * n * H, n, H, H, 1e-5f, D.cln[e].g, D.cln[e].b,
@@ -613,7 +620,8 @@ static int dit_embed_context(alcm_model* m, const float* ctx, int B, float* cemb
 static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const float* cemb, const float* w_emb,
                        float* eps, int B, int T, void* ws, size_t wsb, hipStream_t s) {
   const DitW& D = m->dit;
-  const int split = m->split;
+  const int split = prec_of(m, false);
+  const int pff = prec_of(m, true);  // GEGLU FFN convs: 89% of the DiT FLOPs
   const int H = D.hidden, E = 1 + D.ctx_tokens, L = E + T;
   if (B <= 0 || T <= 0) return set_error(ALCM_E_INVALID, "dit_forward: empty batch");
   if (L > D.max_len)
@@ -678,11 +686,11 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       o.pad = D.ff_k / 2;
       o.pro = Pro{blk.ln3.g, blk.ln3.b, 0, w.mean, w.rstd, 0};
       o.geglu = 1;
-      ALCM_TRY(conv(s, split, B, L, uv, blk.ff0, ocl(w.g, L, 4 * H), o));
+      ALCM_TRY(conv(s, pff, B, L, uv, blk.ff0, ocl(w.g, L, 4 * H), o));
       ConvOpts o2;
       o2.pad = D.ff_k / 2;
       o2.res = ur;
-      ALCM_TRY(conv(s, split, B, L, cl(w.g, L, 4 * H), blk.ff2, uo, o2));
+      ALCM_TRY(conv(s, pff, B, L, cl(w.g, L, 4 * H), blk.ff2, uo, o2));
     }
     {
       ConvOpts o;
@@ -734,13 +742,13 @@ static VaeWs plan_vae(const VaeW& V, Bump& bp, int B, int T) {
 }
 
 // ResnetBlock1D (autoencoder1d.py:212-235): out = x' + conv2(swish(GN(conv1(swish(GN(x))))))
-static int vae_res(hipStream_t s, int split, int B, int T, const ResW& r, const float* x, float* tmp, float* sc,
-                   float* out, VaeWs& w) {
+static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& r, const float* x, float* tmp,
+                   float* sc, float* out, VaeWs& w) {
   ALCM_TRY(group_norm_affine(x, B, T, r.cin, (int64_t)T * r.cin, r.cin, 32, 1e-6f, r.n1.g, r.n1.b, w.gsc, w.gsh, s));
   ConvOpts o1;
   o1.pad = 1;
   o1.pro = Pro{w.gsc, w.gsh, r.cin, nullptr, nullptr, ACT_SILU};
-  ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.c1, ocl(tmp, T, r.cout), o1));
+  ALCM_TRY(conv(s, pk3, B, T, cl(x, T, r.cin), r.c1, ocl(tmp, T, r.cout), o1));
   ALCM_TRY(group_norm_affine(tmp, B, T, r.cout, (int64_t)T * r.cout, r.cout, 32, 1e-6f, r.n2.g, r.n2.b, w.gsc, w.gsh, s));
   const float* resid = x;
   if (r.has_nin) {
@@ -751,13 +759,14 @@ static int vae_res(hipStream_t s, int split, int B, int T, const ResW& r, const 
   o2.pad = 1;
   o2.pro = Pro{w.gsc, w.gsh, r.cout, nullptr, nullptr, ACT_SILU};
   o2.res = Res{resid, (int64_t)T * r.cout, r.cout, 1};
-  return conv(s, split, B, T, cl(tmp, T, r.cout), r.c2, ocl(out, T, r.cout), o2);
+  return conv(s, pk3, B, T, cl(tmp, T, r.cout), r.c2, ocl(out, T, r.cout), o2);
 }
 
 static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel, int B, int T, void* ws, size_t wsb,
                       hipStream_t s) {
   const VaeW& V = m->vae;
-  const int split = m->split;
+  const int split = prec_of(m, false);
+  const int pk3 = prec_of(m, true);  // k3 ResnetBlock1D / upsample convs
   if (B <= 0 || T <= 0) return set_error(ALCM_E_INVALID, "vae_decode: empty batch");
   Bump bp(ws, wsb);
   VaeWs w = plan_vae(V, bp, B, T);
@@ -777,7 +786,7 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
     ALCM_TRY(conv(s, split, B, T, cl(w.d, T, V.z_ch), V.conv_in, ocl(w.a, T, C), o));
   }
   float* h = w.a;
-  ALCM_TRY(vae_res(s, split, B, T, V.mid1, h, w.b, nullptr, h, w));
+  ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid1, h, w.b, nullptr, h, w));
   // AttnBlock1D (autoencoder1d.py:259-278): single head over T, logit scale C^-1/2
   {
     ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, V.attn_n.g, V.attn_n.b, w.gsc, w.gsh, s));
@@ -795,7 +804,7 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
     g.acc_scale = 1.0f / sqrtf((float)C);
     g.out_scale = 1.f;
     g.out = w.S; g.o_st = Tp; g.o_sc = 1; g.o_zs1 = (int64_t)T * Tp; g.out_rows_per_batch = T; g.out_step = 1;
-    g.split = split;
+    g.prec = split;
     ALCM_TRY(gemm(g, s));
     ALCM_TRY(softmax_rows(w.S, B * T, T, Tp, s));
     alcm_gemm_args p;
@@ -807,22 +816,22 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
     p.b.zs1 = (int64_t)T * 3 * C;
     p.acc_scale = 1.f; p.out_scale = 1.f;
     p.out = w.c; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
-    p.split = split;
+    p.prec = split;
     ALCM_TRY(gemm(p, s));
     ConvOpts oo;
     oo.res = Res{h, (int64_t)T * C, C, 1};
     ALCM_TRY(conv(s, split, B, T, cl(w.c, T, C), V.attn_out, ocl(h, T, C), oo));
   }
-  ALCM_TRY(vae_res(s, split, B, T, V.mid2, h, w.b, nullptr, h, w));
+  ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid2, h, w.b, nullptr, h, w));
   int Tc = T;
   float* spare = w.c;  // third full buffer for channel-changing blocks
   for (int lvl = (int)V.mult.size() - 1; lvl >= 0; --lvl) {
     for (const ResW& r : V.lv[lvl]) {
       if (r.has_nin) {
-        ALCM_TRY(vae_res(s, split, B, Tc, r, h, w.b, w.d, spare, w));
+        ALCM_TRY(vae_res(s, split, pk3, B, Tc, r, h, w.b, w.d, spare, w));
         std::swap(h, spare);
       } else {
-        ALCM_TRY(vae_res(s, split, B, Tc, r, h, w.b, nullptr, h, w));
+        ALCM_TRY(vae_res(s, split, pk3, B, Tc, r, h, w.b, nullptr, h, w));
       }
       C = r.cout;
     }
@@ -831,7 +840,7 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
       ConvOpts o;
       o.pad = 1;
       o.up = 2;
-      ALCM_TRY(conv(s, split, B, 2 * Tc, cl(h, Tc, C), V.up[lvl], ocl(spare, 2 * Tc, C), o));
+      ALCM_TRY(conv(s, pk3, B, 2 * Tc, cl(h, Tc, C), V.up[lvl], ocl(spare, 2 * Tc, C), o));
       std::swap(h, spare);
       Tc *= 2;
     }
@@ -883,14 +892,14 @@ static int amp(hipStream_t s, int split, const ActW& a, const ConvW& w, const fl
   g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.Cout = w.w.rows; g.ksize = w.w.taps; g.dil = dil;
   g.pad = (w.w.taps * dil - dil) / 2;
   g.bias = w.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate; g.out_scale = out_scale;
-  g.split = split;
+  g.prec = split;
   return amp_conv(g, s);
 }
 
 static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, int M, void* ws, size_t wsb,
                            hipStream_t s) {
   const VocW& G = m->voc;
-  const int split = m->split;
+  const int split = prec_of(m, false);
   if (B <= 0 || M <= 0) return set_error(ALCM_E_INVALID, "bigvgan_forward: empty batch");
   Bump bp(ws, wsb);
   VocWs w = plan_voc(G, bp, B, M);
@@ -909,8 +918,12 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   float* u = w.y;
   float* rb = w.rb;
   float* y = w.t;
-  for (const StageW& S : G.st) {
+  for (size_t si = 0; si < G.st.size(); ++si) {
+    const StageW& S = G.st[si];
     const int To = T * S.rate;
+    // AMPBlock convs of the three wide stages (C = 768/384/192 for the reference config, ~96% of the
+    // BigVGAN FLOPs) may run as fp16 MFMAs; the narrow tail, upsamplers, conv_pre/post stay split
+    const int pamp = prec_of(m, si < 3);
     // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188)
     for (int r = 0; r < S.rate; ++r) {
       ConvOpts o;
@@ -926,8 +939,8 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
       if (amp_fusable(S.cout)) {
         for (size_t l = 0; l < A.dil.size(); ++l) {
           const bool last = l + 1 == A.dil.size();
-          ALCM_TRY(amp(s, split, A.act[2 * l], A.c1[l], cur, y, B, To, A.dil[l], nullptr, 1.f, 0, 0));
-          ALCM_TRY(amp(s, split, A.act[2 * l + 1], A.c2[l], y, last ? x : rb, B, To, 1, cur, last ? inv : 1.f,
+          ALCM_TRY(amp(s, pamp, A.act[2 * l], A.c1[l], cur, y, B, To, A.dil[l], nullptr, 1.f, 0, 0));
+          ALCM_TRY(amp(s, pamp, A.act[2 * l + 1], A.c2[l], y, last ? x : rb, B, To, 1, cur, last ? inv : 1.f,
                        last && j > 0, 0));
           cur = rb;
         }
@@ -938,7 +951,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
         ConvOpts o1;
         o1.dil = A.dil[l];
         o1.pad = (A.k * A.dil[l] - A.dil[l]) / 2;
-        ALCM_TRY(conv(s, split, B, To, cl(w.a, To, S.cout), A.c1[l], ocl(y, To, S.cout), o1));
+        ALCM_TRY(conv(s, pamp, B, To, cl(w.a, To, S.cout), A.c1[l], ocl(y, To, S.cout), o1));
         ALCM_TRY(act1d(s, A.act[2 * l + 1], y, w.a, B, To, S.cout));
         ConvOpts o2;
         o2.pad = (A.k - 1) / 2;
@@ -948,7 +961,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
           o2.out_scale = inv;
           o2.accumulate = j > 0;
         }
-        ALCM_TRY(conv(s, split, B, To, cl(w.a, To, S.cout), A.c2[l], ocl(last ? x : rb, To, S.cout), o2));
+        ALCM_TRY(conv(s, pamp, B, To, cl(w.a, To, S.cout), A.c2[l], ocl(last ? x : rb, To, S.cout), o2));
         cur = rb;
       }
     }
@@ -981,12 +994,16 @@ extern "C" int alcm_check_device(int dev) {
 }
 
 extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, const alcm_named_tensor* tensors,
-                                 int n_tensors, int split, alcm_model** out) {
+                                 int n_tensors, int policy, alcm_model** out) {
   if (!out || (n_tensors > 0 && !tensors)) return set_error(ALCM_E_INVALID, "model_create: null argument");
   *out = nullptr;
   alcm_model* m = new alcm_model();
   m->kind = kind;
-  m->split = split ? 1 : 0;
+  if (policy < ALCM_POLICY_BF16 || policy > ALCM_POLICY_MIXED) {
+    delete m;
+    return set_error(ALCM_E_INVALID, "model_create: unknown precision policy");
+  }
+  m->policy = policy;
   try {
     Ingest I(m, tensors, n_tensors);
     if (kind == ALCM_MODEL_DIT) build_dit(I, iconfig, n_iconfig);
@@ -1016,7 +1033,14 @@ extern "C" size_t alcm_model_weight_bytes(const alcm_model* m) { return m ? m->w
 
 extern "C" int alcm_model_set_split(alcm_model* m, int split) {
   if (!m) return set_error(ALCM_E_INVALID, "null model");
-  m->split = split ? 1 : 0;
+  m->policy = split ? ALCM_POLICY_SPLIT : ALCM_POLICY_BF16;
+  return 0;
+}
+
+extern "C" int alcm_model_set_precision(alcm_model* m, int policy) {
+  if (!m) return set_error(ALCM_E_INVALID, "null model");
+  if (policy < ALCM_POLICY_BF16 || policy > ALCM_POLICY_MIXED) return set_error(ALCM_E_INVALID, "unknown policy");
+  m->policy = policy;
   return 0;
 }
 

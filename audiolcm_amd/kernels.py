@@ -25,10 +25,18 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def _prec(split: bool, prec: Optional[int]) -> int:
+    """MFMA operand precision code: explicit `prec` (_hip.PREC_*) or split -> PREC_SPLIT / PREC_BF16."""
+    if prec is not None:
+        assert prec in (_hip.PREC_BF16, _hip.PREC_SPLIT, _hip.PREC_F16), prec
+        return int(prec)
+    return _hip.PREC_SPLIT if split else _hip.PREC_BF16
+
+
 @dataclass
 class PackedWeight:
-    """bf16 hi/lo [rows][Kpad] GEMM operand (K index = tap*cpad + ci)."""
-    data: torch.Tensor  # uint16 (2, rows, kpad) on device
+    """[rows][Kpad] GEMM operand planes bf16 hi, bf16 lo, fp16 (K index = tap*cpad + ci)."""
+    data: torch.Tensor  # int16 (3, rows, kpad) on device
     rows: int
     cin: int
     cpad: int
@@ -54,7 +62,7 @@ def pack_conv_weight(w: torch.Tensor, transposed: bool = False, stride: int = 1,
         taps = k
     cpad = _round_up(cin, 8)
     kpad = _round_up(taps * cpad, BK)
-    out = torch.empty((2, cout, kpad), dtype=torch.int16, device=w.device)
+    out = torch.empty((3, cout, kpad), dtype=torch.int16, device=w.device)
     check(lib().alcm_pack_conv_weight(ptr(w), cout, cin, k, cpad, kpad, int(transposed), stride, phase, ptr(out),
                                       stream_handle()), "pack_conv_weight")
     return PackedWeight(out, cout, cin, cpad, taps, kpad)
@@ -78,7 +86,8 @@ def gemm(args: _hip.GemmArgs) -> None:
 def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, padding: int = 0,
            dilation: int = 1, upsample: int = 1, split: bool = True, channels_last: bool = False,
            act: int = 0, residual: Optional[torch.Tensor] = None, packed: Optional[PackedWeight] = None,
-           prologue: Optional[dict] = None, window: bool = True, tile_n: int = 0) -> torch.Tensor:
+           prologue: Optional[dict] = None, window: bool = True, tile_n: int = 0,
+           prec: Optional[int] = None) -> torch.Tensor:
     """F.conv1d(x, w, bias, padding=padding, dilation=dilation) on the MFMA implicit GEMM.
 
     x is (B, Cin, T) (reference NCT layout) or, with channels_last, (B, T, Cin); the result
@@ -126,7 +135,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             g.r_sb, g.r_sc, g.r_st = r.stride()
     g.out = ptr(out)
     g.out_rows_per_batch, g.out_step, g.out_off = Tout, 1, 0
-    g.split = int(split)
+    g.prec = _prec(split, prec)
     g.disable_window = int(not window)
     g.tile_n = tile_n
     gemm(g)
@@ -134,7 +143,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def conv_transpose1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
-                     split: bool = True) -> torch.Tensor:
+                     split: bool = True, prec: Optional[int] = None) -> torch.Tensor:
     """F.conv_transpose1d on NCT input as ``stride`` phase convolutions."""
     B, Cin, T = x.shape
     _, Cout, K = w.shape
@@ -158,21 +167,22 @@ def conv_transpose1d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tens
         g.out = ptr(out)
         g.o_sb, g.o_st, g.o_sc = Cout * Tout, 1, Tout
         g.out_rows_per_batch, g.out_step, g.out_off = T, stride, o
-        g.split = int(split)
+        g.prec = _prec(split, prec)
         gemm(g)
     return out
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, split: bool = True,
-           act: int = 0) -> torch.Tensor:
+           act: int = 0, prec: Optional[int] = None) -> torch.Tensor:
     """F.linear on (..., K) rows."""
     shp = x.shape
     x2 = x.reshape(-1, shp[-1]).contiguous()
-    y = conv1d(x2.unsqueeze(0), w.unsqueeze(-1), bias, split=split, channels_last=True, act=act)
+    y = conv1d(x2.unsqueeze(0), w.unsqueeze(-1), bias, split=split, channels_last=True, act=act, prec=prec)
     return y.reshape(*shp[:-1], w.shape[0])
 
 
-def bmm_nt(a: torch.Tensor, b: torch.Tensor, scale: float = 1.0, split: bool = True) -> torch.Tensor:
+def bmm_nt(a: torch.Tensor, b: torch.Tensor, scale: float = 1.0, split: bool = True,
+           prec: Optional[int] = None) -> torch.Tensor:
     """(Z, M, K) x (Z, N, K)^T -> (Z, M, N): the Q K^T product of attention."""
     Z, M, K = a.shape
     N = b.shape[1]
@@ -188,12 +198,12 @@ def bmm_nt(a: torch.Tensor, b: torch.Tensor, scale: float = 1.0, split: bool = T
     g.out = ptr(out)
     g.o_st, g.o_sc, g.o_zs1 = N, 1, M * N
     g.out_rows_per_batch, g.out_step = M, 1
-    g.split = int(split)
+    g.prec = _prec(split, prec)
     gemm(g)
     return out
 
 
-def bmm_nn(p: torch.Tensor, v: torch.Tensor, split: bool = True) -> torch.Tensor:
+def bmm_nn(p: torch.Tensor, v: torch.Tensor, split: bool = True, prec: Optional[int] = None) -> torch.Tensor:
     """(Z, M, K) x (Z, K, N) -> (Z, M, N): the P V product (V read N-contiguous)."""
     Z, M, K = p.shape
     N = v.shape[2]
@@ -214,7 +224,7 @@ def bmm_nn(p: torch.Tensor, v: torch.Tensor, split: bool = True) -> torch.Tensor
     g.out = ptr(out)
     g.o_st, g.o_sc, g.o_zs1 = N, 1, M * N
     g.out_rows_per_batch, g.out_step = M, 1
-    g.split = int(split)
+    g.prec = _prec(split, prec)
     gemm(g)
     return out
 
@@ -303,7 +313,8 @@ def sincos_embedding(v: torch.Tensor, freqs: torch.Tensor, scale: float, cos_fir
 def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int, padding: int,
              act: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]] = None,
              residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
-             accumulate_into: Optional[torch.Tensor] = None, split: bool = True) -> torch.Tensor:
+             accumulate_into: Optional[torch.Tensor] = None, split: bool = True,
+             prec: Optional[int] = None) -> torch.Tensor:
     """Fused conv_{k,d}(Activation1d(x)) on channels-last (B, T, C) for C in {24, 48, 96}.
 
     act = (alpha, beta, up_filter, down_filter) of the SnakeBeta Activation1d (None: no activation)."""
@@ -325,7 +336,7 @@ def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], 
     a.bias = ptr(bias)
     a.res = ptr(residual.contiguous()) if residual is not None else None
     out = accumulate_into if accumulate_into is not None else torch.empty((B, T, pw.rows), device=x_cl.device)
-    a.out, a.out_act, a.accumulate, a.out_scale, a.split = ptr(out), out_act, int(accumulate_into is not None), \
-        out_scale, int(split)
+    a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
+        out_scale, _prec(split, prec)
     check(lib().alcm_amp_conv(C.byref(a), stream_handle()), "amp_conv")
     return out

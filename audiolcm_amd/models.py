@@ -41,13 +41,26 @@ def _state_to_named(state: Mapping[str, torch.Tensor], extra: Optional[Mapping[s
     return arr, keep
 
 
+def policy_code(split) -> int:
+    """Precision policy from a bool (split / bf16) or a name in _hip.POLICIES."""
+    if isinstance(split, str):
+        if split not in _hip.POLICIES:
+            raise ValueError(f"unknown precision policy {split!r}; expected one of {sorted(_hip.POLICIES)}")
+        return _hip.POLICIES[split]
+    return _hip.POLICY_SPLIT if split else _hip.POLICY_BF16
+
+
 class _HipModel:
     KIND = -1
 
-    def __init__(self, split: bool = True):
+    def __init__(self, split=True):
         self._handle = C.c_void_p(None)
-        self.split = bool(split)
+        self.policy = policy_code(split)
         self._ws: Dict[tuple, torch.Tensor] = {}
+
+    @property
+    def split(self) -> bool:
+        return self.policy != _hip.POLICY_BF16
 
     # -- weights -----------------------------------------------------------------------------
     def _iconfig(self) -> List[int]:
@@ -64,16 +77,19 @@ class _HipModel:
         ic = self._iconfig()
         icarr = (C.c_int * len(ic))(*ic)
         h = C.c_void_p(None)
-        check(lib().alcm_model_create(self.KIND, icarr, len(ic), arr, len(arr), int(self.split), C.byref(h)),
+        check(lib().alcm_model_create(self.KIND, icarr, len(ic), arr, len(arr), self.policy, C.byref(h)),
               f"{type(self).__name__}.load_state_dict")
         del keep
         self._handle = h
         return self
 
-    def set_split(self, split: bool):
-        self.split = bool(split)
+    def set_split(self, split):
+        """True/False (bf16x3 everywhere / bf16 everywhere) or a policy name "bf16" | "split" | "mixed"."""
+        self.policy = policy_code(split)
         if self._handle:
-            check(lib().alcm_model_set_split(self._handle, int(self.split)))
+            check(lib().alcm_model_set_precision(self._handle, self.policy))
+
+    set_precision = set_split
 
     @property
     def loaded(self) -> bool:

@@ -53,8 +53,11 @@ int alcm_version(void);
 int alcm_check_device(int dev);
 
 /* ---------------------------------------------------------------- generic MFMA GEMM / implicit-GEMM conv1d
- * C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), bf16 MFMA (v_mfma_f32_16x16x32_bf16) with fp32
- * accumulate; split=1 uses the 3-term bf16 split (hi*hi + hi*lo + lo*hi) for fp32-level accuracy. */
+ * C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), MFMA with fp32 accumulate.  Operand precision `prec`:
+ *   ALCM_PREC_BF16  (0) one v_mfma_f32_16x16x32_bf16 (operands rounded to bf16)
+ *   ALCM_PREC_SPLIT (1) 3-term bf16 split (hi*hi + hi*lo + lo*hi): fp32-level accuracy, 3x the MFMA work
+ *   ALCM_PREC_F16   (2) one v_mfma_f32_16x16x32_f16 (operands rounded to fp16) */
+enum { ALCM_PREC_BF16 = 0, ALCM_PREC_SPLIT = 1, ALCM_PREC_F16 = 2 };
 enum { ALCM_OPND_ACT = 0, ALCM_OPND_ACT_T = 1, ALCM_OPND_WEIGHT = 2 };
 
 typedef struct alcm_operand {
@@ -64,7 +67,8 @@ typedef struct alcm_operand {
    *      t_src = t + tap*dil - pad (up == 2: nearest-x2 upsampled input, t_up = t + tap*dil - pad,
    *      t_src = t_up/2), zero outside [0, T_in) / ci >= C_in / k >= ksize*Cpad.
    * ACT_T: element (n, k) at ptr + k*st + n*sc, valid k < T_in, n < rows.
-   * WEIGHT: packed bf16 [rows][Kpad] hi plane at ptr, lo plane at ptr + w_lo_off (elements). */
+   * WEIGHT: packed [rows][Kpad] planes: bf16 hi at ptr, bf16 lo at ptr + w_lo_off, fp16 at
+ *         ptr + 2*w_lo_off (elements; w_lo_off = rows*Kpad as written by alcm_pack_conv_weight). */
   int64_t sb, st, sc;
   int T_in, C_in, Cpad, ksize, dil, pad, up;
   int rows_per_batch; /* ACT: rows m -> (b = m / rows_per_batch, t = m % rows_per_batch) */
@@ -98,16 +102,16 @@ typedef struct alcm_gemm_args {
   float* out;
   int64_t o_sb, o_st, o_sc, o_zs1, o_zs2;
   int out_rows_per_batch, out_step, out_off;
-  int split;
+  int prec;           /* ALCM_PREC_* */
   int disable_window; /* 1: never use the window-conv kernel (testing / A-B timing) */
   int tile_n;         /* 0: automatic; 64 / 128: force the N tile of the window-conv kernel */
 } alcm_gemm_args;
 
 int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream);
 
-/* pack a conv/linear weight W[co][ci][k] (fp32, DEVICE) into the bf16 hi/lo [Cout][Kpad] layout with
- * K index = tap*Cpad + ci. transposed=1 takes a ConvTranspose1d weight [ci][co][k] and a phase
- * (stride s, phase r) selecting taps j = r + s*(Q-1-tap), Q = k/s. out must hold 2*Cout*Kpad u16. */
+/* pack a conv/linear weight W[co][ci][k] (fp32, DEVICE) into three [Cout][Kpad] planes (bf16 hi, bf16 lo,
+ * fp16) with K index = tap*Cpad + ci. transposed=1 takes a ConvTranspose1d weight [ci][co][k] and a phase
+ * (stride s, phase r) selecting taps j = r + s*(Q-1-tap), Q = k/s. out must hold 3*Cout*Kpad u16. */
 int alcm_pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed,
                           int stride, int phase, void* out, alcm_stream_t stream);
 
@@ -148,7 +152,7 @@ typedef struct alcm_amp_args {
   float* out;
   int out_act, accumulate;
   float out_scale;
-  int split;
+  int prec; /* ALCM_PREC_* */
 } alcm_amp_args;
 int alcm_amp_conv(const alcm_amp_args* args, alcm_stream_t stream);
 
@@ -182,11 +186,18 @@ typedef struct alcm_model alcm_model;
 /* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL decoder, 2 = BigVGAN.
  * iconfig/fconfig: see DESIGN.md §C-ABI (hyper-parameters from configs/audiolcm.yaml / bigvgan json) */
 enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2 };
+/* policy: ALCM_POLICY_* (below) */
 int alcm_model_create(int kind, const int* iconfig, int n_iconfig, const alcm_named_tensor* tensors,
-                      int n_tensors, int split, alcm_model** out);
+                      int n_tensors, int policy, alcm_model** out);
 int alcm_model_destroy(alcm_model* m);
 size_t alcm_model_weight_bytes(const alcm_model* m);
 int alcm_model_set_split(alcm_model* m, int split);
+/* per-layer precision policy: ALCM_POLICY_BF16 every contraction bf16; ALCM_POLICY_SPLIT every contraction
+ * bf16x3 (fp32 parity); ALCM_POLICY_MIXED fp16 single MFMA on the layers the parity budget allows
+ * (DiT GEGLU FFN convs, VAE k3 ResnetBlock/upsample convs, BigVGAN stage 0-2 AMPBlock convs: DESIGN.md §3),
+ * bf16x3 elsewhere.  alcm_model_set_split(m, s) == set_precision(m, s ? SPLIT : BF16). */
+enum { ALCM_POLICY_BF16 = 0, ALCM_POLICY_SPLIT = 1, ALCM_POLICY_MIXED = 2 };
+int alcm_model_set_precision(alcm_model* m, int policy);
 
 /* DiT.  x (B,C_lat,T) NCT, t (B,) int64, ctx (B,154,1024), w_emb (B,256) -> eps (B,C_lat,T) NCT.
  * cemb_cache: (B,154,hidden) device buffer filled by alcm_dit_embed_context (step-invariant, hoisted). */

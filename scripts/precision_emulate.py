@@ -104,5 +104,68 @@ def main():
                 print(f"{name:22s} wscale={int(ws)}  wav rel-L2 {err:.2e}", flush=True)
 
 
+
+
+def run_latent_mel(policy, Wd, Wv, ctx, xT, noise):
+    """DiT sampler + VAE decode in float64 with conv/linear operands rounded per policy:
+    policy keys: 'dit_ffn' (k=9 GEGLU convs), 'dit_other' (all other DiT convs/linears),
+    'vae_conv' (k=3 ResnetBlock/upsample convs), 'vae_other'."""
+    state = {"model": "dit"}
+    real_conv, real_lin = F.conv1d, F.linear
+
+    def grp(w):
+        if state["model"] == "dit":
+            return "dit_ffn" if (w.dim() == 3 and w.shape[-1] == 9) else "dit_other"
+        return "vae_conv" if (w.dim() == 3 and w.shape[-1] == 3) else "vae_other"
+
+    def conv1d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+        a_f, w_f = policy.get(grp(w), ("f32", "f32"))
+        return real_conv(rnd(x.to(w.dtype), a_f), rnd(w, w_f), b, stride, padding, dilation, groups)
+
+    def linear(x, w, b=None):
+        a_f, w_f = policy.get(grp(w), ("f32", "f32"))
+        return real_lin(rnd(x.to(w.dtype), a_f), rnd(w, w_f), b)
+
+    ns = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("_")})
+    ns.conv1d, ns.linear = conv1d, linear
+    old_F, O.F = O.F, ns
+    try:
+        eps_fn = lambda x, t, w: O.dit_forward(Wd, x, t, ctx, w)
+        z = O.lcm_sample(eps_fn, ctx, xT, noise, 2, 5.0)
+        state["model"] = "vae"
+        mel = O.vae_decode(Wv, z)
+    finally:
+        O.F = old_F
+    return z, mel
+
+
+def main_dit_vae():
+    torch.set_num_threads(max(1, min(8, len(os.sched_getaffinity(0)))))
+    Wd = {k: v.double() for k, v in recipe.dit_state(0).items()}
+    Wv = {k: v.double() for k, v in recipe.vae_state(0).items()}
+    g = np.load(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "e2e_S2_B2.npz"))
+    ctx = recipe.synthetic_context(2).double()
+    xT, noise = torch.from_numpy(g["x_T"]).double(), torch.from_numpy(g["noise"]).double()
+    with torch.no_grad():
+        z0, m0 = run_latent_mel({}, Wd, Wv, ctx, xT, noise)
+        print(f"fp64 vs fixture: latent {float((z0.float() - torch.from_numpy(g['latent'])).norm() / z0.norm()):.2e}")
+        cases = {
+            "dit ffn f16": {"dit_ffn": ("f16", "f16")},
+            "dit ffn bf16": {"dit_ffn": ("bf16", "bf16")},
+            "dit other f16": {"dit_other": ("f16", "f16")},
+            "dit all f16": {"dit_ffn": ("f16", "f16"), "dit_other": ("f16", "f16")},
+            "vae conv f16": {"vae_conv": ("f16", "f16")},
+            "vae all f16": {"vae_conv": ("f16", "f16"), "vae_other": ("f16", "f16")},
+            "dit ffn + vae conv f16": {"dit_ffn": ("f16", "f16"), "vae_conv": ("f16", "f16")},
+        }
+        for name, pol in cases.items():
+            z, m = run_latent_mel(pol, Wd, Wv, ctx, xT, noise)
+            print(f"{name:26s} latent {float((z - z0).norm() / z0.norm()):.2e}  mel {float((m - m0).norm() / m0.norm()):.2e}",
+                  flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "ditvae":
+        main_dit_vae()
+    else:
+        main()

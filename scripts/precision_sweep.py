@@ -26,12 +26,12 @@ def main():
     g = dict(np.load(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "e2e_S2_B2.npz")))
     pipe = AudioLCMPipeline.from_recipe(0)
     ctx = recipe.synthetic_context(2).cuda()
-    for dit, vae, voc in itertools.product((True, False), repeat=3):
+    for dit, vae, voc in itertools.product(("split", "mixed", "bf16"), repeat=3):
         pipe.model.unet.diffusion_model.set_split(dit)
         pipe.model.first_stage_model.set_split(vae)
         pipe.vocoder.set_split(voc)
         out = pipe.generate(ctx, seeds=[0, 1], steps=2)
-        print(f"dit={'split' if dit else 'bf16 '} vae={'split' if vae else 'bf16 '} voc={'split' if voc else 'bf16 '}"
+        print(f"dit={dit:5s} vae={vae:5s} voc={voc:5s}"
               f"  latent {rel(out['latent'].cpu(), g['latent']):.2e}  mel {rel(out['mel'].cpu(), g['mel']):.2e}"
               f"  wav {rel(out['wav'].cpu(), g['wav']):.2e}", flush=True)
 

@@ -1,7 +1,7 @@
 """Op-level parity of the HIP kernels (through the C-ABI) against plain fp32 PyTorch on CPU.
 
 Tolerances: split (bf16x3) MFMA mode is fp32-accurate -> relative L2 <= 2e-5;
-plain bf16 MFMA mode -> relative L2 <= 1.5e-2.
+plain bf16 MFMA mode -> relative L2 <= 1.5e-2; fp16 MFMA mode (prec=2) -> relative L2 <= 2e-3.
 """
 import numpy as np
 import pytest
@@ -14,6 +14,9 @@ pytestmark = pytest.mark.gpu
 
 SPLIT_TOL = 2e-5
 BF16_TOL = 1.5e-2
+F16_TOL = 2e-3
+PRECS = [1, 0, 2]                     # _hip.PREC_SPLIT, PREC_BF16, PREC_F16
+TOL = {1: SPLIT_TOL, 0: BF16_TOL, 2: F16_TOL}
 
 
 @pytest.fixture(scope="module")
@@ -46,29 +49,29 @@ def dev(t):
     (3, 64, 129, 48, 7, 9, 3, True),     # window-conv, BN=64 tile, T not a tile multiple
     (1, 32, 5, 64, 3, 1, 1, True),       # window-conv, T shorter than the halo
 ])
-@pytest.mark.parametrize("split", [True, False])
-def test_conv1d(K, B, Cin, T, Cout, k, pad, dil, cl, split):
+@pytest.mark.parametrize("prec", PRECS)
+def test_conv1d(K, B, Cin, T, Cout, k, pad, dil, cl, prec):
     x = _r((B, Cin, T), 1)
     w = _r((Cout, Cin, k), 2, 1.0 / np.sqrt(Cin * k))
     b = _r((Cout,), 3, 0.1)
     ref = F.conv1d(x, w, b, padding=pad, dilation=dil)
     xin = x.permute(0, 2, 1).contiguous() if cl else x
-    y = K.conv1d(dev(xin), dev(w), dev(b), padding=pad, dilation=dil, split=split, channels_last=cl).cpu()
+    y = K.conv1d(dev(xin), dev(w), dev(b), padding=pad, dilation=dil, prec=prec, channels_last=cl).cpu()
     if cl:
         y = y.permute(0, 2, 1)
     assert y.shape == ref.shape
-    assert rel_l2(y.numpy(), ref.numpy()) < (SPLIT_TOL if split else BF16_TOL)
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
 
 
-@pytest.mark.parametrize("split", [True, False])
-def test_window_conv_matches_tap_loader(K, split):
+@pytest.mark.parametrize("prec", PRECS)
+def test_window_conv_matches_tap_loader(K, prec):
     """The window-conv kernel and the tap-by-tap implicit GEMM give the same result (same bf16 operands)."""
     x = _r((2, 300, 128), 40)
     w = _r((192, 128, 7), 41, 0.03)
     b = _r((192,), 42, 0.1)
-    y1 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, split=split, channels_last=True)
-    y2 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, split=split, channels_last=True, window=False)
-    assert rel_l2(y1.cpu().numpy(), y2.cpu().numpy()) < (1e-6 if split else 1e-5)
+    y1 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, prec=prec, channels_last=True)
+    y2 = K.conv1d(dev(x), dev(w), dev(b), padding=9, dilation=3, prec=prec, channels_last=True, window=False)
+    assert rel_l2(y1.cpu().numpy(), y2.cpu().numpy()) < (1e-6 if prec == 1 else 1e-5)
 
 
 def test_conv1d_upsample_nearest(K):
@@ -179,8 +182,8 @@ def test_activation1d_long(K):
 @pytest.mark.parametrize("C,k,dil,T,act,res", [
     (24, 11, 5, 700, True, True), (48, 7, 3, 333, True, False), (96, 3, 1, 150, True, True),
     (96, 11, 1, 40, False, False), (24, 3, 1, 5, True, True)])
-@pytest.mark.parametrize("split", [True, False])
-def test_amp_conv_fused(K, C, k, dil, T, act, res, split):
+@pytest.mark.parametrize("prec", PRECS)
+def test_amp_conv_fused(K, C, k, dil, T, act, res, prec):
     """Fused Activation1d + conv (BigVGAN narrow stages) vs oracle Activation1d then F.conv1d (+ residual)."""
     from oracle import alcm_oracle as O
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
@@ -194,8 +197,8 @@ def test_amp_conv_fused(K, C, k, dil, T, act, res, split):
     ref = F.conv1d(h, w, bias, dilation=dil, padding=(k * dil - dil) // 2) + (r if res else 0)
     y = K.amp_conv(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(bias), dil, (k * dil - dil) // 2,
                    act=(dev(a), dev(bt), f, f) if act else None,
-                   residual=dev(r.permute(0, 2, 1).contiguous()) if res else None, split=split).cpu().permute(0, 2, 1)
-    assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if split else BF16_TOL)
+                   residual=dev(r.permute(0, 2, 1).contiguous()) if res else None, prec=prec).cpu().permute(0, 2, 1)
+    assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
 
 
 def test_amp_conv_post_tanh_and_accumulate(K):
