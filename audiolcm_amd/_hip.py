@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("ALCM_LIB", os.path.join(HERE, "libaudiolcm_hip.so"))
 ALCM_OPND_ACT, ALCM_OPND_ACT_T, ALCM_OPND_WEIGHT = 0, 1, 2
 ALCM_MODEL_DIT, ALCM_MODEL_VAE, ALCM_MODEL_BIGVGAN = 0, 1, 2
 ACT_NONE, ACT_SILU, ACT_GELU_ERF, ACT_GELU_TANH, ACT_TANH = 0, 1, 2, 3, 4
-PREC_BF16, PREC_SPLIT, PREC_F16 = 0, 1, 2              # per-launch MFMA operand precision
+PREC_BF16, PREC_SPLIT, PREC_F16, PREC_F16W2 = 0, 1, 2, 3   # per-launch MFMA operand precision
 POLICY_BF16, POLICY_SPLIT, POLICY_MIXED = 0, 1, 2      # per-model precision policy
 POLICIES = {"bf16": POLICY_BF16, "split": POLICY_SPLIT, "mixed": POLICY_MIXED}
 
@@ -49,6 +49,14 @@ class AmpArgs(C.Structure):
                 ("alpha_exp", fp), ("inv_beta", fp), ("up_filter", fp), ("down_filter", fp), ("w", vp),
                 ("w_lo_off", i64), ("kpad", C.c_int), ("Cout", C.c_int), ("ksize", C.c_int), ("dil", C.c_int),
                 ("pad", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
+                ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int),
+                ("seg_tiles", C.c_int)]
+
+
+class OpConvArgs(C.Structure):
+    _fields_ = [("a", vp), ("a_lo_off", i64), ("B", C.c_int), ("T", C.c_int), ("C", C.c_int), ("Cp", C.c_int),
+                ("ksize", C.c_int), ("dil", C.c_int), ("pad", C.c_int), ("w", vp), ("w_lo_off", i64),
+                ("kpad", C.c_int), ("N", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
                 ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int)]
 
 
@@ -76,6 +84,8 @@ _SIGS = [
     ("alcm_softmax_rows", C.c_int, [fp, C.c_int, C.c_int, i64, vp]),
     ("alcm_activation1d", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, i64, i64, fp, fp, fp, fp, vp]),
     ("alcm_amp_conv", C.c_int, [C.POINTER(AmpArgs), vp]),
+    ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
+    ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_lcm_step_cfg", C.c_int, [fp, fp, fp, C.c_float, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_sincos_embedding", C.c_int, [fp, C.c_float, fp, C.c_int, C.c_int, C.c_int, fp, vp]),

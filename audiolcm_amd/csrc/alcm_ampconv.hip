@@ -1,18 +1,24 @@
 // Fused anti-aliased activation + dilated conv1d for BigVGAN's narrow stages (C <= 96).
 //
 // One AMPBlock1 half-layer is  y = conv_{k,d}( Activation1d(x) ) + bias [+ residual]
-// (vocoder/bigvgan/models.py:72-81, alias_free_torch/act.py:23-27).  At C = 24/48/96 these
-// layers are HBM-bound; as separate kernels they moved x through HBM three times and re-read
-// the conv input k times through L2.  Here one workgroup owns BM output rows x all channels:
-//   1. the conv input window rows [t0 - pad, t0 + BM + (k-1)d - pad) are produced by the
-//      Activation1d of x (up-FIR -> SnakeBeta -> down-FIR, evaluated from L1/L2-resident x),
-//      zero outside [0, T) (the conv's zero padding), split to bf16 hi/lo straight into LDS;
-//   2. the implicit GEMM runs over K = (tap, channel) reading A fragments from the window at
-//      row offset tap*d and B fragments (packed weights, a few KB, L1/L2-hot) straight from
-//      global memory: no barrier inside the K loop;
-//   3. epilogue: bias, activation (tanh for conv_post), residual, scale/accumulate (mean of
-//      the three resblocks), store.
-// HBM traffic per layer: read x once (+ halo), write y once (+ residual read).
+// (vocoder/bigvgan/models.py:72-81, alias_free_torch/act.py:23-27), and conv_post is the same
+// shape with Cout = 1 and tanh (models.py:201-203).  At C = 24/48/96 these layers move 1-2 GB
+// through HBM per launch at B=32 and are HBM/VALU-bound once the MFMA part is efficient.
+//
+// Streaming design (one workgroup = 4 waves = one batch row b and a segment of R*BM output rows):
+//   * the conv input window lives in an LDS *ring* of WRING rows (>= BM + (k-1)d) holding
+//     Activation1d(x) as MFMA operand planes (bf16 hi/lo for PREC_SPLIT, fp16 for PREC_F16);
+//     each sub-tile of BM output rows computes only the BM rows that enter the window
+//     (the first sub-tile also the (k-1)d halo), so the activation runs ~once per element;
+//   * the implicit GEMM runs over K = (tap, channel): A fragments are read from the ring at
+//     row offset tap*d (per lane, modulo WRING), B (packed weights, L2-resident) is staged
+//     per K-step into a double-buffered LDS tile shared by the 4 waves (one barrier per step);
+//   * epilogue: bias, activation (tanh for conv_post), residual (prefetched before the K loop),
+//     scale / accumulate (mean of the three resblocks), store.
+// HBM traffic per layer: read x once (+ halo at segment starts), write y once (+ residual read).
+#include <cstdio>
+#include <cstdlib>
+
 #include "alcm_common.h"
 #include "alcm_internal.h"
 
@@ -39,9 +45,11 @@ struct AmpDev {
   int64_t o_sb;
   int out_act, accumulate;
   float out_scale;
-  int tiles_per_batch;
+  int segs_per_batch, seg_tiles;
+  int ablate;  // diagnostics only (env ALCM_AMP_ABLATE): bit0 skip activation, bit1 skip K loop, bit2 skip epilogue
 };
 
+// sin^2(x) with a Cody-Waite reduction to [-pi/4, pi/4] and minimax sin/cos polynomials (fp32, ~1 ulp)
 __device__ __forceinline__ float amp_sin_sq(float x) {
   const float k = rintf(x * 0.63661977236758134f);
   float r = fmaf(-k, 1.5703125f, x);
@@ -55,22 +63,22 @@ __device__ __forceinline__ float amp_sin_sq(float x) {
   return v * v;
 }
 
-constexpr int AR = 16;  // activation outputs per work item
-
-// Activation1d of channel c for window rows [w0, w0+AR): input time tt = tb + w, 0 outside [0,T).
-template <bool ACT>
-__device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st, int T, int tb, int w0, int wr,
-                                        float ea, float ib, const Taps12A& f, float (&o)[AR]) {
-  const int j0 = tb + w0;
+// Activation1d (UpSample1d -> SnakeBeta -> DownSample1d, act.py:23-27) of one channel for AR
+// consecutive output times j0 .. j0+AR-1 (xc = x + b*sb + c, row stride st); 0 outside [0, T)
+// (that is the conv's zero padding, not the activation's replicate padding).
+template <int AR, bool ACT>
+__device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st, int T, int j0, float ea, float ib,
+                                        const Taps12A& f, float (&o)[AR]) {
   if (!ACT) {
 #pragma unroll
     for (int r = 0; r < AR; ++r) {
       const int j = j0 + r;
-      o[r] = (j >= 0 && j < T && w0 + r < wr) ? xc[(int64_t)j * st] : 0.f;
+      o[r] = (j >= 0 && j < T) ? xc[(int64_t)j * st] : 0.f;
     }
     return;
   }
   if (j0 >= 6 && j0 + AR + 6 <= T) {
+    // interior: replicate padding never reached; upsampled sample q pairs with input window win
     float win[AR + 12];
 #pragma unroll
     for (int i = 0; i < AR + 12; ++i) win[i] = xc[(int64_t)(j0 - 6 + i) * st];
@@ -95,10 +103,11 @@ __device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st
     }
     return;
   }
+  // edges: explicit replicate padding of the up (pad 5) and down (pad 5/6) filters
   for (int r = 0; r < AR; ++r) {
     const int j = j0 + r;
     float acc = 0.f;
-    if (j >= 0 && j < T && w0 + r < wr) {
+    if (j >= 0 && j < T) {
       for (int k = 0; k < 12; ++k) {
         int m = 2 * j + k - 5;
         m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
@@ -117,180 +126,357 @@ __device__ __forceinline__ void act_run(const float* __restrict__ xc, int64_t st
   }
 }
 
-// BM output rows per workgroup (4 waves x BM/4 rows), all Cout (<= TN*16) columns.
-constexpr int AMP_WAVES = 8;  // 512-thread workgroups: one activation item per thread, more waves in flight
-template <int BM, int TN, int CPAD, int PREC, bool ACT>
-__global__ __launch_bounds__(64 * AMP_WAVES) void amp_conv_kernel(const AmpDev P) {
-  constexpr int NT = 64 * AMP_WAVES;
-  constexpr int WROWS = BM / AMP_WAVES;  // output rows per wave
-  constexpr int TM = WROWS / 16;
-  static_assert(TM >= 1 && WROWS % 16 == 0, "BM must give each wave a multiple of 16 rows");
-  constexpr int S = CPAD + 8 + ((8 - (CPAD + 8) % 32 + 32) % 32);  // row stride (bf16) == 8 mod 32
-  constexpr int WR_MAX = BM + 64;
-  constexpr bool SPLIT = PREC == PREC_SPLIT;
-  constexpr int NP = SPLIT ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) __bf16 Wn[NP][WR_MAX * S];
+// LDS ring row stride (bf16 elements) == 8 mod 32: the 16 rows of an A-fragment read land on
+// distinct 16-byte slots of each ds_read_b128 lane group for any start row
+template <int CPAD>
+struct RingRow {
+  static constexpr int S = CPAD + 8 + ((8 - (CPAD + 8) % 32 + 32) % 32);
+};
+
+// B tile in LDS: NT rows x 32 k (64 B) per plane, 16-B chunk kq of row r at slot kq ^ ((r >> 2) & 2)
+__device__ __forceinline__ int bt_off(int r, int kq) { return r * 32 + ((kq ^ ((r >> 2) & 2)) << 3); }
+
+// Interior Activation1d from an LDS fp32 stage of x: xr points at the staged row of input time j0 - 6
+// (channel c, row stride CPAD); the caller guarantees 6 <= j0 and j0 + AR + 6 <= T.
+template <int AR, int CPAD>
+__device__ __forceinline__ void act_run_lds(const float* xr, float ea, float ib, const Taps12A& f, float (&o)[AR]) {
+  float win[AR + 12];
+#pragma unroll
+  for (int i = 0; i < AR + 12; ++i) win[i] = xr[i * CPAD];
+  float sv[2 * AR + 10];
+#pragma unroll
+  for (int q = 0; q < 2 * AR + 10; ++q) {
+    float u = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int k = 2 * kk + (q & 1);
+      u = fmaf(f.up[k], win[(q - k) / 2 + 6], u);
+    }
+    u *= 2.0f;
+    sv[q] = u + ib * amp_sin_sq(u * ea);
+  }
+#pragma unroll
+  for (int r = 0; r < AR; ++r) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc = fmaf(f.dn[k], sv[2 * r + k], acc);
+    o[r] = acc;
+  }
+}
+
+// CPAD = Cin; wave grid WGM x WGN, each wave TM x TN 16x16 tiles; BM = WGM*TM*16 rows per sub-tile,
+// NT = WGN*TN*16 >= Cout columns; AR activation rows per work item; WRING ring rows (power of 2);
+// XR rows of x staged per activation chunk (XR >= BM + 12: one chunk per sub-tile after the first).
+//
+// Per sub-tile jt the workgroup runs  [activation of BM new rows from the x stage -> ring] ->
+// [K loop; meanwhile the x rows of sub-tile jt+1 and this sub-tile's residual are loaded into
+// registers] -> [epilogue through an LDS tile] -> [prefetched x -> x stage], so the HBM latency of
+// the next activation and of the residual hides behind this sub-tile's MFMAs.
+template <int CPAD, int WGM, int WGN, int TM, int TN, int AR, int WRING, int XR, int PREC, bool ACT>
+__global__ __launch_bounds__(256) void amp_conv_kernel(const AmpDev P) {
+  constexpr int BM = WGM * TM * 16;
+  constexpr int NT = WGN * TN * 16;
+  constexpr int NPA = PREC == PREC_SPLIT ? 2 : 1;                           // activation planes
+  constexpr int NPB = (PREC == PREC_SPLIT || PREC == PREC_F16W2) ? 2 : 1;  // weight planes
+  constexpr int S = RingRow<CPAD>::S;
+  constexpr int BCH = NT * 4;  // 16-B chunks per B plane per K-step
+  constexpr int BPER = (BCH + 255) / 256;
+  constexpr int OTS = NT + 4;  // output-tile row stride (floats): spreads the acc writes over banks
+  constexpr int CH = XR - 12;  // activation rows per x stage
+  constexpr int C4 = CPAD / 4;
+  constexpr int XPER = (XR * C4 + 255) / 256;         // prefetched float4 of x per thread
+  constexpr int RPER = (BM * NT / 4 + 255) / 256;     // prefetched float4 of the residual per thread
+  static_assert(WGM * WGN == 4, "4 waves");
+  static_assert((WRING & (WRING - 1)) == 0 && WRING >= BM + 64, "ring must hold BM + max halo rows");
+  static_assert(CPAD % 4 == 0 && CH >= BM, "x stage must hold one sub-tile of new rows");
+  // scratch is time-shared: x stage (activation) / B double buffer (K loop) / output tile (epilogue)
+  constexpr int SB_B = 2 * NPB * NT * 32 * 2, SB_X = XR * CPAD * 4, SB_O = BM * OTS * 4;
+  constexpr int SB = SB_B > SB_X ? (SB_B > SB_O ? SB_B : SB_O) : (SB_X > SB_O ? SB_X : SB_O);
+  __shared__ __attribute__((aligned(16))) __bf16 ring[NPA][WRING * S];
+  __shared__ __attribute__((aligned(16))) char scratch[SB];
+  __bf16* bsb = reinterpret_cast<__bf16*>(scratch);  // [2][NPB][NT*32]
+  float* xs = reinterpret_cast<float*>(scratch);     // [XR][CPAD]
+  float* ot = reinterpret_cast<float*>(scratch);     // [BM][OTS]
+  auto bs = [&](int buf, int pl) { return bsb + (buf * NPB + pl) * NT * 32; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x / P.tiles_per_batch;
-  const int t0 = (blockIdx.x - b * P.tiles_per_batch) * BM;
-  const int WR = BM + (P.ksize - 1) * P.dil;
-  const int tb = t0 - P.pad;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int b = blockIdx.x / P.segs_per_batch;
+  const int seg = blockIdx.x - b * P.segs_per_batch;
+  const int t_begin = seg * P.seg_tiles * BM;
+  const int halo = (P.ksize - 1) * P.dil;
+  const int tw0 = t_begin - P.pad;  // input time of relative window row 0
   const float* xb = P.x + (int64_t)b * P.x_sb;
+  const int Kr = P.ksize * CPAD;
+  const int nks = P.kpad / 32;
+  const int Cout = P.Cout;
+  const bool vec_out = (Cout % 4) == 0;
 
-  // ---- 1. activation window -> LDS (bf16 hi/lo)
-  const int runs = (WR + AR - 1) / AR;
-  const int items = runs * P.Cin;
-  // residual of this lane's output elements: issued before the activation phase so its latency hides
-  float resv[TM][4][TN];
+  // B staging (per K-step: rows n < Cout of the packed weight, k0 .. k0+31; zero rows beyond Cout)
+  const u16* bsrc[BPER];
+  bool bok[BPER];
+#pragma unroll
+  for (int i = 0; i < BPER; ++i) {
+    const int c = tid + i * 256;
+    const int n = c >> 2;
+    bok[i] = c < BCH && n < Cout;
+    bsrc[i] = P.w + (int64_t)(bok[i] ? n : 0) * P.kpad + (c & 3) * 8;
+  }
+  uint4 bh[BPER], bl[BPER];
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+      bh[i] = make_uint4(0, 0, 0, 0);
+      bl[i] = make_uint4(0, 0, 0, 0);
+      if (bok[i]) {
+        bh[i] = *reinterpret_cast<const uint4*>(bsrc[i] + k0);
+        if (NPB == 2) bl[i] = *reinterpret_cast<const uint4*>(bsrc[i] + k0 + P.w_lo);
+      }
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+      const int c = tid + i * 256;
+      if (c >= BCH) continue;
+      const int off = bt_off(c >> 2, c & 3);
+      *reinterpret_cast<uint4*>(bs(buf, 0) + off) = bh[i];
+      if (NPB == 2) *reinterpret_cast<uint4*>(bs(buf, NPB - 1) + off) = bl[i];
+    }
+  };
+  auto put_ring = [&](int row, int c, float v) {
+    const int slot = row & (WRING - 1);
+    if constexpr (PREC == PREC_F16 || PREC == PREC_F16W2) {
+      ring[0][slot * S + c] = __builtin_bit_cast(__bf16, (_Float16)v);
+    } else {
+      const __bf16 h = (__bf16)v;
+      ring[0][slot * S + c] = h;
+      if (NPA == 2) ring[NPA - 1][slot * S + c] = (__bf16)(v - (float)h);
+    }
+  };
+  // x rows [jx0, jx0 + nrows) -> registers (rows outside [0, T) read as 0)
+  float4 xp[XPER];
+  auto load_x = [&](int jx0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int e = tid + i * 256;
+      const int rr = e / C4, c4 = e - rr * C4;
+      const int j = jx0 + rr;
+      xp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rr < nrows && j >= 0 && j < P.T) xp[i] = *reinterpret_cast<const float4*>(xb + (int64_t)j * CPAD + c4 * 4);
+    }
+  };
+  auto store_x = [&](int nrows) {
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int e = tid + i * 256;
+      if (e < nrows * C4) *reinterpret_cast<float4*>(xs + e * 4) = xp[i];
+    }
+  };
+  // activation of window rows [w, w + rows) from the x stage (staged row 0 = input time tw0 + w - 6)
+  auto act_chunk = [&](int w, int rows) {
+    const int runs = (rows + AR - 1) / AR;
+    for (int e = tid; e < runs * CPAD; e += 256) {
+      const int c = e % CPAD, run = e / CPAD;
+      const int w0 = w + run * AR;
+      const int j0 = tw0 + w0;
+      float o[AR];
+      if (!ACT) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) o[r] = xs[(run * AR + r + 6) * CPAD + c];
+      } else if (j0 >= 6 && j0 + AR + 6 <= P.T) {
+        act_run_lds<AR, CPAD>(xs + run * AR * CPAD + c, P.aexp[c], P.ibeta[c], P.f, o);
+      } else {
+        act_run<AR, true>(xb + c, CPAD, P.T, j0, P.aexp[c], P.ibeta[c], P.f, o);
+      }
+#pragma unroll
+      for (int r = 0; r < AR; ++r)
+        if (w0 + r < w + rows) put_ring(w0 + r, c, o[r]);
+    }
+  };
+
+  // prologue: the first sub-tile's window rows [0, BM + halo), staged in chunks of CH rows
+  int have = 0;
   {
+    const int need = BM + halo;
+    for (int w = 0; w < need; w += CH) {
+      const int rows = min(CH, need - w);
+      load_x(tw0 + w - 6, rows + 12);
+      store_x(rows + 12);
+      __syncthreads();
+      if (!(P.ablate & 1)) act_chunk(w, rows);
+      __syncthreads();
+    }
+    have = need;
+  }
+
+  for (int jt = 0; jt < P.seg_tiles; ++jt) {
+    const int t0 = t_begin + jt * BM;
+    if (t0 >= P.T) break;
+    const bool next = jt + 1 < P.seg_tiles && t0 + BM < P.T;
+    if (jt > 0) {
+      // BM new rows [have, have + BM), staged at the end of the previous sub-tile
+      if (!(P.ablate & 1)) act_chunk(have, BM);
+      have += BM;
+      __syncthreads();  // ring rows visible; x stage free for the B buffers
+    }
+
+    // ---- K loop, with the next sub-tile's x rows and this sub-tile's residual prefetched
+    load_b(0);
+    if (next) load_x(tw0 + have - 6, BM + 12);
+    float4 rp[RPER];
+    const int mrows = min(BM, P.T - t0);
+    const float* rbp = P.res ? P.res + (int64_t)b * P.r_sb + (int64_t)t0 * Cout : nullptr;
+    if (vec_out) {
+      const int q4 = Cout / 4;
+#pragma unroll
+      for (int i = 0; i < RPER; ++i) {
+        const int e = tid + i * 256;
+        rp[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rbp && e < mrows * q4) rp[i] = *reinterpret_cast<const float4*>(rbp + (int64_t)e * 4);
+      }
+    }
+    store_b(0);
+    __syncthreads();
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int mrow = jt * BM + wm * TM * 16 + (lane & 15);  // relative window row of this lane's A rows (tap 0)
+    for (int ks = 0; ks < ((P.ablate & 2) ? 0 : nks); ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < nks) load_b((ks + 1) * 32);
+      const int k8 = ks * 32 + 8 * (lane >> 4);
+      const bool kok = k8 < Kr;
+      const int tap = k8 / CPAD;
+      const int ci = k8 - tap * CPAD;
+      bf16x8 ah[TM], al[NPA == 2 ? TM : 1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int off = ((mrow + i * 16 + tap * P.dil) & (WRING - 1)) * S + ci;
+        if (kok) {
+          ah[i] = *reinterpret_cast<const bf16x8*>(&ring[0][off]);
+          if (NPA == 2) al[i] = *reinterpret_cast<const bf16x8*>(&ring[NPA - 1][off]);
+        } else {
+          ah[i] = bf16x8{};
+          if (NPA == 2) al[i] = bf16x8{};
+        }
+      }
+      bf16x8 fh[TN], fl[NPB == 2 ? TN : 1];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int off = bt_off(wn * TN * 16 + j * 16 + (lane & 15), lane >> 4);
+        fh[j] = *reinterpret_cast<const bf16x8*>(bs(cur, 0) + off);
+        if (NPB == 2) fl[j] = *reinterpret_cast<const bf16x8*>(bs(cur, NPB - 1) + off);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (PREC == PREC_SPLIT) {
+            acc[i][j] = mfma16<PREC_BF16>(al[i], fh[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_BF16>(ah[i], fl[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_BF16>(ah[i], fh[j], acc[i][j]);
+          } else if constexpr (PREC == PREC_F16W2) {
+            acc[i][j] = mfma16<PREC_F16>(ah[i], fl[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_F16>(ah[i], fh[j], acc[i][j]);
+          } else {
+            acc[i][j] = mfma16<PREC>(ah[i], fh[j], acc[i][j]);
+          }
+        }
+      if (ks + 1 < nks) store_b(cur ^ 1);
+      __syncthreads();  // also orders this sub-tile's ring reads before the next sub-tile's writes
+    }
+    if (P.ablate & 2) __syncthreads();
+
+    // ---- epilogue: acc (+bias, out_act) -> LDS tile -> coalesced 16-B rows (+res, *scale, +out)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = t0 + wave * WROWS + i * 16 + (lane >> 4) * 4 + r;
+        const int m = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int n = j * 16 + (lane & 15);
-          resv[i][r][j] = (P.res && t < P.T && n < P.Cout) ? P.res[(int64_t)b * P.r_sb + (int64_t)t * P.Cout + n] : 0.f;
+          const int n = wn * TN * 16 + j * 16 + (lane & 15);
+          float v = acc[i][j][r];
+          if (P.bias && n < Cout) v += P.bias[n];
+          if (P.out_act) v = alcm_act(v, P.out_act);
+          ot[m * OTS + n] = v;
         }
       }
-  }
-  for (int e = tid; e < items; e += NT) {
-    const int c = e % P.Cin, run = e / P.Cin;
-    float o[AR];
-    act_run<ACT>(xb + c, P.Cin, P.T, tb, run * AR, WR, ACT ? P.aexp[c] : 0.f, ACT ? P.ibeta[c] : 0.f, P.f, o);
-    // rows in [WR, runs*AR) are never read by the MFMAs; WR_MAX covers them, so no per-row guard
+    __syncthreads();
+    float* ob = P.out + (int64_t)b * P.o_sb + (int64_t)t0 * Cout;
+    if (!(P.ablate & 4)) {
+      if (vec_out) {
+        const int q4 = Cout / 4;
 #pragma unroll
-    for (int r = 0; r < AR; ++r) {
-      const int w = run * AR + r;
-      if constexpr (PREC == PREC_F16) {
-        Wn[0][w * S + c] = __builtin_bit_cast(__bf16, (_Float16)o[r]);
-      } else {
-        const __bf16 h = (__bf16)o[r];
-        Wn[0][w * S + c] = h;
-        if (SPLIT) Wn[NP - 1][w * S + c] = (__bf16)(o[r] - (float)h);
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- 2. implicit GEMM over K = (tap, channel), A from the window, B straight from global
-  const int Kr = P.ksize * CPAD;
-  const int row_base = wave * WROWS + (lane & 15);
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const u16* wrow[TN];
-  bool nok[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = j * 16 + (lane & 15);
-    nok[j] = n < P.Cout;
-    wrow[j] = P.w + (int64_t)(nok[j] ? n : 0) * P.kpad + 8 * (lane >> 4);
-  }
-  // B fragments are prefetched one K-step ahead (L1/L2 latency hidden behind the MFMAs)
-  bf16x8 nbh[TN], nbl[SPLIT ? TN : 1];
-  auto load_b = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      uint4 h = make_uint4(0, 0, 0, 0), l = make_uint4(0, 0, 0, 0);
-      if (nok[j]) {
-        h = *reinterpret_cast<const uint4*>(wrow[j] + k0);
-        if (SPLIT) l = *reinterpret_cast<const uint4*>(wrow[j] + k0 + P.w_lo);
-      }
-      nbh[j] = __builtin_bit_cast(bf16x8, h);
-      if (SPLIT) nbl[j] = __builtin_bit_cast(bf16x8, l);
-    }
-  };
-  load_b(0);
-  for (int k0 = 0; k0 < P.kpad; k0 += 32) {
-    bf16x8 bh[TN], bl[SPLIT ? TN : 1];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bh[j] = nbh[j];
-      if (SPLIT) bl[j] = nbl[j];
-    }
-    if (k0 + 32 < P.kpad) load_b(k0 + 32);
-    const int k8 = k0 + 8 * (lane >> 4);
-    const bool kok = k8 < Kr;
-    const int tap = k8 / CPAD;
-    const int ci = k8 - tap * CPAD;
-    bf16x8 ah[TM], al[SPLIT ? TM : 1];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (kok) {
-        const int off = (row_base + i * 16 + tap * P.dil) * S + ci;
-        ah[i] = *reinterpret_cast<const bf16x8*>(&Wn[0][off]);
-        if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(&Wn[NP - 1][off]);
-      } else {
-        ah[i] = bf16x8{};
-        if (SPLIT) al[i] = bf16x8{};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (SPLIT) {
-          acc[i][j] = mfma16<PREC>(al[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma16<PREC>(ah[i], bl[j], acc[i][j]);
+        for (int i = 0; i < RPER; ++i) {
+          const int e = tid + i * 256;
+          if (e >= mrows * q4) continue;
+          const int m = e / q4, n = (e - m * q4) * 4;
+          float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+          v.x += rp[i].x; v.y += rp[i].y; v.z += rp[i].z; v.w += rp[i].w;
+          v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+          if (P.accumulate) {
+            const float4 pv = *reinterpret_cast<const float4*>(ob + (int64_t)e * 4);
+            v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+          }
+          *reinterpret_cast<float4*>(ob + (int64_t)e * 4) = v;
         }
-        acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
+      } else {
+        for (int e = tid; e < mrows * Cout; e += 256) {
+          const int m = e / Cout, n = e - m * Cout;
+          float v = ot[m * OTS + n];
+          if (rbp) v += rbp[e];
+          v *= P.out_scale;
+          if (P.accumulate) v += ob[e];
+          ob[e] = v;
+        }
       }
-  }
-
-  // ---- 3. epilogue
-#pragma clang loop unroll(full)
-  for (int i = 0; i < TM; ++i) {
-#pragma clang loop unroll(full)
-    for (int r = 0; r < 4; ++r) {
-      const int t = t0 + wave * WROWS + i * 16 + (lane >> 4) * 4 + r;
-      if (t >= P.T) continue;
-#pragma clang loop unroll(full)
-      for (int j = 0; j < TN; ++j) {
-        const int n = j * 16 + (lane & 15);
-        if (n >= P.Cout) continue;
-        float v = acc[i][j][r];
-        if (P.bias) v += P.bias[n];
-        if (P.out_act) v = alcm_act(v, P.out_act);
-        v += resv[i][r][j];
-        v *= P.out_scale;
-        float* o = P.out + (int64_t)b * P.o_sb + (int64_t)t * P.Cout + n;
-        if (P.accumulate) v += *o;
-        *o = v;
-      }
+    }
+    __syncthreads();  // output tile (scratch) becomes the next sub-tile's x stage
+    if (next) {
+      store_x(BM + 12);
+      __syncthreads();
     }
   }
 }
 
-template <int BM, int TN, int CPAD, int PREC>
+template <int CPAD, int WGM, int WGN, int TM, int TN, int AR, int WRING, int XR, int PREC>
 static void launch_amp_p(const AmpDev& Q, dim3 grid, bool act, hipStream_t s) {
-  if (act) hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, PREC, true>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
-  else hipLaunchKernelGGL((amp_conv_kernel<BM, TN, CPAD, PREC, false>), grid, dim3(64 * AMP_WAVES), 0, s, Q);
+  if (act)
+    hipLaunchKernelGGL((amp_conv_kernel<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC, true>), grid, dim3(256), 0, s,
+                       Q);
+  else
+    hipLaunchKernelGGL((amp_conv_kernel<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC, false>), grid, dim3(256), 0, s,
+                       Q);
 }
 
-template <int BM, int TN, int CPAD>
-static void launch_amp(const AmpDev& P, int B, int prec, bool act, hipStream_t s) {
+template <int CPAD, int WGM, int WGN, int TM, int TN, int AR, int WRING, int XR>
+static void launch_amp(const AmpDev& P, int B, int prec, bool act, int force_tiles, hipStream_t s) {
+  constexpr int BM = WGM * TM * 16;
   AmpDev Q = P;
-  Q.tiles_per_batch = (P.T + BM - 1) / BM;
-  dim3 grid(B * Q.tiles_per_batch);
+  const int tiles = (P.T + BM - 1) / BM;
+  // sub-tiles per workgroup: ~2.5k workgroups over the chip (>= 8 per CU), few halo recomputes
+  int st = force_tiles > 0 ? force_tiles : std::max(1, (int)(((int64_t)tiles * B + 2559) / 2560));
+  st = std::min(st, tiles);
+  Q.seg_tiles = st;
+  Q.segs_per_batch = (tiles + st - 1) / st;
+  dim3 grid(B * Q.segs_per_batch);
   void* tok = prof_start(s);
-  if (prec == PREC_SPLIT) launch_amp_p<BM, TN, CPAD, PREC_SPLIT>(Q, grid, act, s);
-  else if (prec == PREC_F16) launch_amp_p<BM, TN, CPAD, PREC_F16>(Q, grid, act, s);
-  else launch_amp_p<BM, TN, CPAD, PREC_BF16>(Q, grid, act, s);
-  const bool split = prec == PREC_SPLIT;
+  if (prec == PREC_SPLIT) launch_amp_p<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC_SPLIT>(Q, grid, act, s);
+  else if (prec == PREC_F16) launch_amp_p<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC_F16>(Q, grid, act, s);
+  else if (prec == PREC_F16W2) launch_amp_p<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC_F16W2>(Q, grid, act, s);
+  else launch_amp_p<CPAD, WGM, WGN, TM, TN, AR, WRING, XR, PREC_BF16>(Q, grid, act, s);
   if (tok) {
     char name[128];
-    std::snprintf(name, sizeof(name), "alcm::amp_conv_kernel<%d, %d, %d, %d, %s>", BM, TN, CPAD, prec,
-                  act ? "true" : "false");
+    std::snprintf(name, sizeof(name), "alcm::amp_conv_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %s>", CPAD, WGM,
+                  WGN, TM, TN, AR, WRING, XR, prec, act ? "true" : "false");
     const double elems = (double)B * P.T;
     const double flops = 2.0 * elems * P.Cout * (double)P.ksize * P.Cin;
     const double bytes = elems * (P.Cin + P.Cout * (1 + (P.res ? 1 : 0) + (P.accumulate ? 1 : 0))) * 4.0 +
-                         (double)P.Cout * P.kpad * 2.0 * (split ? 2 : 1);
+                         (double)P.Cout * P.kpad * 2.0 * (prec == PREC_SPLIT || prec == PREC_F16W2 ? 2 : 1);
     prof_stop(tok, s, name, flops, bytes);
   }
 }
@@ -301,9 +487,14 @@ int amp_conv(const alcm_amp_args& a, hipStream_t s) {
   if (a.act && (!a.alpha_exp || !a.inv_beta || !a.up_filter || !a.down_filter))
     return set_error(ALCM_E_INVALID, "amp_conv: activation parameters missing");
   if ((a.ksize - 1) * a.dil > 64) return set_error(ALCM_E_INVALID, "amp_conv: receptive field too large");
+  if (a.pad < 0 || a.pad > (a.ksize - 1) * a.dil) return set_error(ALCM_E_INVALID, "amp_conv: bad padding");
   const int cpad = round_up(a.Cin, 8);
   if (a.kpad < a.ksize * cpad || a.kpad % 32) return set_error(ALCM_E_INVALID, "amp_conv: kpad mismatch");
   if (a.x == a.out) return set_error(ALCM_E_INVALID, "amp_conv: in-place not supported");
+  if (a.prec < PREC_BF16 || a.prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "amp_conv: bad prec");
+  if (a.seg_tiles < 0) return set_error(ALCM_E_INVALID, "amp_conv: seg_tiles must be >= 0");
+  if ((int64_t)a.B * a.T * std::max(a.Cin, a.Cout) >= (1ll << 31))
+    return set_error(ALCM_E_INVALID, "amp_conv: problem too large");
   AmpDev P{};
   P.x = a.x; P.x_sb = (int64_t)a.T * a.Cin; P.T = a.T; P.Cin = a.Cin;
   P.aexp = a.alpha_exp; P.ibeta = a.inv_beta;
@@ -312,19 +503,23 @@ int amp_conv(const alcm_amp_args& a, hipStream_t s) {
       P.f.up[k] = a.up_filter[k];
       P.f.dn[k] = a.down_filter[k];
     }
-  if (a.prec < PREC_BF16 || a.prec > PREC_F16) return set_error(ALCM_E_INVALID, "amp_conv: bad prec");
-  // PREC_F16 reads the packed weight's fp16 plane (ptr + 2*w_lo_off)
-  P.w = (const u16*)a.w + (a.prec == PREC_F16 ? 2 * a.w_lo_off : 0); P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.Cout = a.Cout; P.ksize = a.ksize;
+  // PREC_F16 / PREC_F16W2 read the packed weight's fp16 hi (+ lo) planes (ptr + 2*w_lo_off, + 3*w_lo_off)
+  P.w = (const u16*)a.w + ((a.prec == PREC_F16 || a.prec == PREC_F16W2) ? 2 * a.w_lo_off : 0);
+  P.w_lo = a.w_lo_off;
+  P.kpad = a.kpad; P.Cout = a.Cout; P.ksize = a.ksize;
   P.dil = a.dil; P.pad = a.pad; P.bias = a.bias; P.res = a.res; P.r_sb = (int64_t)a.T * a.Cout;
   P.out = a.out; P.o_sb = (int64_t)a.T * a.Cout; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
-  const int split = a.prec;
+  const int prec = a.prec;
   const bool act = a.act != 0;
+  const int ft = a.seg_tiles;
+  if (const char* ab = std::getenv("ALCM_AMP_ABLATE")) P.ablate = std::atoi(ab);
   if (cpad != a.Cin) return set_error(ALCM_E_INVALID, "amp_conv: Cin must be a multiple of 8");
-  if (a.Cin == 24 && a.Cout <= 16) launch_amp<256, 1, 24>(P, a.B, split, act, s);
-  else if (a.Cin == 24 && a.Cout <= 32) launch_amp<256, 2, 24>(P, a.B, split, act, s);
-  else if (a.Cin == 48 && a.Cout <= 48) launch_amp<128, 3, 48>(P, a.B, split, act, s);
-  else if (a.Cin == 96 && a.Cout <= 96) launch_amp<128, 6, 96>(P, a.B, split, act, s);
+  //                                            CPAD WGM WGN TM TN AR WRING XR
+  if (a.Cin == 24 && a.Cout <= 16) launch_amp<24, 4, 1, 2, 1, 16, 256, 140>(P, a.B, prec, act, ft, s);
+  else if (a.Cin == 24 && a.Cout <= 32) launch_amp<24, 4, 1, 2, 2, 16, 256, 140>(P, a.B, prec, act, ft, s);
+  else if (a.Cin == 48 && a.Cout <= 48) launch_amp<48, 4, 1, 1, 3, 16, 128, 76>(P, a.B, prec, act, ft, s);
+  else if (a.Cin == 96 && a.Cout <= 96) launch_amp<96, 2, 2, 2, 3, 8, 128, 76>(P, a.B, prec, act, ft, s);
   else return set_error(ALCM_E_INVALID, "amp_conv: unsupported channel count (24/48/96)");
   ALCM_HIP(hipGetLastError());
   return 0;

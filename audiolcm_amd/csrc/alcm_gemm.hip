@@ -781,7 +781,7 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- weight packing (device)
-// W[co][ci][k] fp32 -> planes bf16 hi, bf16 lo, fp16 [co][Kpad], K index = tap*cpad + ci.  For ConvTranspose1d
+// W[co][ci][k] fp32 -> planes bf16 hi, bf16 lo, fp16 hi, fp16 lo [co][Kpad], K index = tap*cpad + ci.  For ConvTranspose1d
 // (weight [ci][co][k], stride s, phase r) tap j = r + s*(Q-1-tap).
 __global__ void pack_weight_kernel(const float* w, int c_out, int c_in, int ksz, int cpad, int kpad, int transposed,
                                    int stride, int phase, u16* out) {
@@ -804,7 +804,9 @@ __global__ void pack_weight_kernel(const float* w, int c_out, int c_in, int ksz,
     const __bf16 l = (__bf16)(v - (float)h);
     out[idx] = __builtin_bit_cast(u16, h);
     out[idx + total] = __builtin_bit_cast(u16, l);
-    out[idx + 2 * total] = __builtin_bit_cast(u16, (_Float16)v);
+    const _Float16 fh = (_Float16)v;
+    out[idx + 2 * total] = __builtin_bit_cast(u16, fh);
+    out[idx + 3 * total] = __builtin_bit_cast(u16, (_Float16)(v - (float)fh));
   }
 }
 

@@ -40,6 +40,10 @@ int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, co
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
 int amp_conv(const alcm_amp_args& a, hipStream_t s);
+int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                    const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                    hipStream_t s);
+int opconv(const alcm_opconv_args& a, hipStream_t s);
 
 bool prof_enabled();
 void* prof_start(hipStream_t s);

@@ -169,15 +169,15 @@ struct Ingest {
   }
   // pack W[co][ci][k] (or ConvTranspose [ci][co][k] phase) into bf16 hi / bf16 lo / fp16 [rows][kpad]
   Packed pack(const std::vector<float>& w, int cout, int cin, int k, int transposed = 0, int stride = 1,
-              int phase = 0) {
+              int phase = 0, int cpad_to = 8) {
     Packed P;
     P.rows = cout;
     P.cin = cin;
-    P.cpad = round_up(cin, 8);
+    P.cpad = round_up(cin, cpad_to);
     P.taps = transposed ? k / stride : k;
     P.kpad = round_up(P.taps * P.cpad, kBK);
     P.lo = (int64_t)cout * P.kpad;
-    P.p = (u16*)dalloc((size_t)3 * cout * P.kpad * sizeof(u16));  // bf16 hi, bf16 lo, fp16 planes
+    P.p = (u16*)dalloc((size_t)4 * cout * P.kpad * sizeof(u16));  // bf16 hi, bf16 lo, fp16 hi, fp16 lo planes
     void* tmp = nullptr;
     if (hipMalloc(&tmp, w.size() * sizeof(float)) != hipSuccess) throw Error(ALCM_E_HIP, "hipMalloc tmp failed");
     (void)hipMemcpy(tmp, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -431,7 +431,8 @@ static void build_voc(Ingest& I, const int* ic, int nic) {
         for (int which = 0; which < 2; ++which) {
           const std::string cp = rp + (which ? "convs2." : "convs1.") + std::to_string(l) + ".";
           ConvW cw;
-          cw.w = I.pack(I.wn(cp, {S.cout, S.cout, A.k}), S.cout, S.cout, A.k);
+          // K = tap*Cp + ci with Cp = round_up(C, 32): the layout of the operand planes alcm_opconv reads
+          cw.w = I.pack(I.wn(cp, {S.cout, S.cout, A.k}), S.cout, S.cout, A.k, 0, 1, 0, 32);
           cw.b = I.upload(I.get(cp + "bias", {S.cout}));
           (which ? A.c2 : A.c1).push_back(cw);
         }
@@ -444,7 +445,7 @@ static void build_voc(Ingest& I, const int* ic, int nic) {
   }
   const int ch = G.st.back().cout;
   G.post_act = build_act(I, "activation_post.", ch);
-  G.post.w = I.pack(I.wn("conv_post.", {1, ch, 7}), 1, ch, 7);
+  G.post.w = I.pack(I.wn("conv_post.", {1, ch, 7}), 1, ch, 7, 0, 1, 0, 32);
   G.post.b = I.upload(I.get("conv_post.bias", {1}));
 }
 
@@ -855,6 +856,8 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
 // ------------------------------------------------------------------ BigVGAN
 struct VocWs {
   float *x, *y, *rb, *a, *t;
+  u16* pl;  // Activation1d output as MFMA operand planes (2 planes of B * T * Cp)
+  int64_t pl_lo;
 };
 static size_t voc_elems(const VocW& G, int M) {
   size_t big = (size_t)M * G.c0;
@@ -867,33 +870,48 @@ static size_t voc_elems(const VocW& G, int M) {
 }
 static VocWs plan_voc(const VocW& G, Bump& bp, int B, int M) {
   const size_t e = (size_t)B * voc_elems(G, M);
+  size_t pe = 0;  // largest B * T * Cp over the AMPBlock stages
+  int T = M;
+  for (const StageW& S : G.st) {
+    T *= S.rate;
+    pe = std::max(pe, (size_t)B * T * round_up(S.cout, 32));
+  }
   VocWs w;
   w.x = bp.take<float>(e);
   w.y = bp.take<float>(e);
   w.rb = bp.take<float>(e);
   w.a = bp.take<float>(e);
   w.t = bp.take<float>(e);
+  w.pl = bp.take<u16>(2 * pe);
+  w.pl_lo = (int64_t)pe;
   return w;
 }
 
-static int act1d(hipStream_t s, const ActW& a, const float* x, float* y, int B, int T, int C) {
-  return activation1d(x, y, B, T, C, (int64_t)T * C, C, a.aexp, a.ibeta, a.fup, a.fdn, s);
+// MFMA precision of the AMPBlock layers of stage si (scripts/precision_emulate.py):
+// mixed policy: fp16 for the three wide stages (~96% of the BigVGAN FLOPs), fp16 activation x fp16 hi+lo
+// weight for the narrow tail (the tail is sensitive to weight rounding, not to activation rounding);
+// conv_post stays bf16x3 (bigvgan_forward)
+static int voc_prec(const alcm_model* m, int si) {
+  if (m->policy == ALCM_POLICY_BF16) return PREC_BF16;
+  if (m->policy == ALCM_POLICY_SPLIT) return PREC_SPLIT;
+  return si < 3 ? PREC_F16 : PREC_F16W2;
 }
 
-static bool amp_fusable(int c) { return c == 24 || c == 48 || c == 96; }
+static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs& w, int B, int T, int C, int prec) {
+  return activation1d_op(x, w.pl, B, T, C, round_up(C, 32), a.aexp, a.ibeta, a.fup, a.fdn, prec, s);
+}
 
-// fused Activation1d + conv (alcm_ampconv.hip) for the narrow BigVGAN stages
-static int amp(hipStream_t s, int split, const ActW& a, const ConvW& w, const float* x, float* out, int B, int T,
-               int dil, const float* res, float out_scale, int accumulate, int out_act) {
-  alcm_amp_args g;
+static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
+                      float* out, float out_scale, int accumulate, int out_act, int prec) {
+  alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
-  g.x = x; g.B = B; g.T = T; g.Cin = w.w.cin;
-  g.act = 1; g.alpha_exp = a.aexp; g.inv_beta = a.ibeta; g.up_filter = a.fup; g.down_filter = a.fdn;
-  g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.Cout = w.w.rows; g.ksize = w.w.taps; g.dil = dil;
-  g.pad = (w.w.taps * dil - dil) / 2;
-  g.bias = w.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate; g.out_scale = out_scale;
-  g.prec = split;
-  return amp_conv(g, s);
+  g.a = w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
+  g.B = B; g.T = T; g.C = cw.w.cin; g.Cp = cw.w.cpad;
+  g.ksize = cw.w.taps; g.dil = dil; g.pad = (cw.w.taps - 1) * dil / 2;
+  g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
+  g.bias = cw.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate;
+  g.out_scale = out_scale; g.prec = prec;
+  return opconv(g, s);
 }
 
 static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, int M, void* ws, size_t wsb,
@@ -921,9 +939,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   for (size_t si = 0; si < G.st.size(); ++si) {
     const StageW& S = G.st[si];
     const int To = T * S.rate;
-    // AMPBlock convs of the three wide stages (C = 768/384/192 for the reference config, ~96% of the
-    // BigVGAN FLOPs) may run as fp16 MFMAs; the narrow tail, upsamplers, conv_pre/post stay split
-    const int pamp = prec_of(m, si < 3);
+    const int pamp = voc_prec(m, (int)si);
     // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188)
     for (int r = 0; r < S.rate; ++r) {
       ConvOpts o;
@@ -931,50 +947,29 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
       ALCM_TRY(conv(s, split, B, T, cl(x, T, S.cin), S.phase[r],
                     Out{u, (int64_t)To * S.cout, S.cout, 1, S.rate, S.off[r]}, o));
     }
-    // x = mean over k in (3,7,11) of AMPBlock1(k, (1,3,5))(u)  (models.py:190-199, 72-81)
+    // x = mean over k in (3,7,11) of AMPBlock1(k, (1,3,5))(u)  (models.py:190-199, 72-81); each half-layer
+    // is Activation1d -> operand planes (alcm_opconv.hip act_op) -> implicit-GEMM conv on the planes
     const float inv = 1.0f / (float)S.rb.size();
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
       const float* cur = u;
-      if (amp_fusable(S.cout)) {
-        for (size_t l = 0; l < A.dil.size(); ++l) {
-          const bool last = l + 1 == A.dil.size();
-          ALCM_TRY(amp(s, pamp, A.act[2 * l], A.c1[l], cur, y, B, To, A.dil[l], nullptr, 1.f, 0, 0));
-          ALCM_TRY(amp(s, pamp, A.act[2 * l + 1], A.c2[l], y, last ? x : rb, B, To, 1, cur, last ? inv : 1.f,
-                       last && j > 0, 0));
-          cur = rb;
-        }
-        continue;
-      }
       for (size_t l = 0; l < A.dil.size(); ++l) {
-        ALCM_TRY(act1d(s, A.act[2 * l], cur, w.a, B, To, S.cout));
-        ConvOpts o1;
-        o1.dil = A.dil[l];
-        o1.pad = (A.k * A.dil[l] - A.dil[l]) / 2;
-        ALCM_TRY(conv(s, pamp, B, To, cl(w.a, To, S.cout), A.c1[l], ocl(y, To, S.cout), o1));
-        ALCM_TRY(act1d(s, A.act[2 * l + 1], y, w.a, B, To, S.cout));
-        ConvOpts o2;
-        o2.pad = (A.k - 1) / 2;
-        o2.res = Res{cur, (int64_t)To * S.cout, S.cout, 1};
         const bool last = l + 1 == A.dil.size();
-        if (last) {
-          o2.out_scale = inv;
-          o2.accumulate = j > 0;
-        }
-        ALCM_TRY(conv(s, pamp, B, To, cl(w.a, To, S.cout), A.c2[l], ocl(last ? x : rb, To, S.cout), o2));
+        ALCM_TRY(act_planes(s, A.act[2 * l], cur, w, B, To, S.cout, pamp));
+        ALCM_TRY(plane_conv(s, A.c1[l], w, B, To, A.dil[l], nullptr, y, 1.f, 0, 0, pamp));
+        ALCM_TRY(act_planes(s, A.act[2 * l + 1], y, w, B, To, S.cout, pamp));
+        ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, last ? x : rb, last ? inv : 1.f, last && j > 0, 0, pamp));
         cur = rb;
       }
     }
     T = To;
   }
   // activation_post -> conv_post k7 -> tanh (models.py:201-203)
-  if (amp_fusable(G.st.back().cout))
-    return amp(s, split, G.post_act, G.post, x, wav, B, T, 1, nullptr, 1.f, 0, ACT_TANH);
-  ALCM_TRY(act1d(s, G.post_act, x, w.a, B, T, G.st.back().cout));
-  ConvOpts o;
-  o.pad = 3;
-  o.act = ACT_TANH;
-  return conv(s, split, B, T, cl(w.a, T, G.st.back().cout), G.post, Out{wav, (int64_t)T, 1, 1, 1, 0}, o);
+  // conv_post maps 24 channels to the waveform: its input rounding shows up 1:1 in the output, so the
+  // mixed policy keeps it bf16x3 (one launch, ~5e-4 of the waveform error budget otherwise)
+  const int ppost = m->policy == ALCM_POLICY_BF16 ? PREC_BF16 : PREC_SPLIT;
+  ALCM_TRY(act_planes(s, G.post_act, x, w, B, T, G.st.back().cout, ppost));
+  return plane_conv(s, G.post, w, B, T, 1, nullptr, wav, 1.f, 0, ACT_TANH, ppost);
 }
 
 }  // namespace alcm

@@ -1,0 +1,555 @@
+// Operand-format path of the BigVGAN AMPBlock convolutions (gfx950).
+//
+// An AMPBlock1 half-layer (vocoder/bigvgan/models.py:72-81) is  y = conv_{k,d}(Activation1d(x)) + b.
+// Here it runs as two kernels:
+//   act_op_kernel   Activation1d (alias_free_torch/act.py:23-27: up-FIR x2 -> SnakeBeta -> down-FIR)
+//                   of the fp32 (B, T, C) tensor, written straight in MFMA operand format: fp16, or
+//                   bf16 hi/lo planes for the bf16x3 split, channels padded to Cp = round_up(C, 32);
+//   opconv_kernel   implicit-GEMM conv1d on those planes: per 32-channel chunk the input window
+//                   rows [t0 - pad, t0 + BM + (k-1)d - pad) are copied once into LDS (double-buffered
+//                   across chunks) and reused by all k taps; the packed weight tile of each (chunk, tap)
+//                   step is prefetched two steps ahead through registers into a double-buffered LDS
+//                   tile, so the L2 latency of the weight stream hides behind two steps of MFMAs.
+// Against the fp32 conv path this halves the conv's A-operand bytes and removes its fp32->bf16
+// conversions; against the fused narrow-stage kernel (alcm_ampconv.hip) it trades one 2-byte
+// round trip of the activation for a K loop free of activation work.
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+
+#include "alcm_common.h"
+#include "alcm_internal.h"
+
+namespace alcm {
+
+struct Taps12O {
+  float up[12], dn[12];
+};
+
+// sin(x)^2: Cody-Waite quadrant reduction + minimax sin/cos on |r| <= pi/4 (~1 ulp, branch-free)
+__device__ __forceinline__ float op_sin_sq(float x) {
+  const float k = rintf(x * 0.63661977236758134f);
+  float r = fmaf(-k, 1.5703125f, x);
+  r = fmaf(-k, 4.837512969970703125e-4f, r);
+  r = fmaf(-k, 7.54978995489188216e-8f, r);
+  const float z = r * r;
+  const float sn = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+  const float cs = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                  4.166664568298827e-2f), z, -0.5f), z, 1.0f);
+  const float v = (((int)k) & 1) ? cs : sn;
+  return v * v;
+}
+
+// ------------------------------------------------------------------ Activation1d -> operand planes
+// thread = (batch, run of AOP_R output rows, channel pair): two channels ride in one float2 so the FIR
+// FMAs issue as v_pk_fma_f32 (half the VALU instructions of a scalar channel); lanes run along channel
+// pairs (8-byte coalesced loads, 4-byte stores of two 16-bit operands).  SnakeBeta's sin^2(z) is
+// 1/2 - cos(2z)/2 with 2z reduced to [-1/2, 1/2] revolutions and the hardware v_cos_f32 (a handful of
+// instructions instead of a ~20-op polynomial).  Pairs at or beyond C write zeros (operand padding).
+constexpr int AOP_R = 16;  // output rows per thread
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// x + h - h*cos(2*pi*r), r = x*ea_rev - rint(x*ea_rev): SnakeBeta with h = inv_beta/2, ea_rev = exp(alpha)/pi
+__device__ __forceinline__ f32x2 snake2(f32x2 u, f32x2 ear, f32x2 h) {
+  const f32x2 z = u * ear;
+  f32x2 r;
+  r.x = z.x - rintf(z.x);
+  r.y = z.y - rintf(z.y);
+  f32x2 c;
+  c.x = __builtin_amdgcn_cosf(r.x);
+  c.y = __builtin_amdgcn_cosf(r.y);
+  return fma2(-h, c, u + h);
+}
+
+template <int PREC>
+__device__ __forceinline__ void op_store2(u16* hi, int64_t lo_off, f32x2 v) {
+  uint32_t wh, wl = 0;
+  if constexpr (PREC == PREC_F16 || PREC == PREC_F16W2) {
+    wh = (uint32_t)__builtin_bit_cast(u16, (_Float16)v.x) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)v.y) << 16);
+  } else {
+    const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+    wh = (uint32_t)__builtin_bit_cast(u16, hx) | ((uint32_t)__builtin_bit_cast(u16, hy) << 16);
+    if (PREC == PREC_SPLIT)
+      wl = (uint32_t)__builtin_bit_cast(u16, (__bf16)(v.x - (float)hx)) |
+           ((uint32_t)__builtin_bit_cast(u16, (__bf16)(v.y - (float)hy)) << 16);
+  }
+  *reinterpret_cast<uint32_t*>(hi) = wh;
+  if (PREC == PREC_SPLIT) *reinterpret_cast<uint32_t*>(hi + lo_off) = wl;
+}
+
+// thread = (batch, run of R output rows, channel pair); lanes run along channel pairs (8-byte coalesced
+// loads, 4-byte stores).  R trades halo work ((2R+10)/R upsampled samples per output) against registers
+// (occupancy): the FIR/snake chains are dependency-bound, so more resident waves matter.
+template <int PREC, int R>
+__global__ __launch_bounds__(256) void act_op_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t y_lo,
+                                                     int T, int C, int Cp, const float* __restrict__ aexp,
+                                                     const float* __restrict__ ibeta, const Taps12O f,
+                                                     uint32_t total, FastDiv pdiv, FastDiv rdiv) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < total; w += gridDim.x * 256u) {
+    uint32_t rb, cpair, b, run;
+    pdiv.divmod(w, rb, cpair);
+    rdiv.divmod(rb, b, run);
+    const int c = 2 * (int)cpair;
+    const int j0 = (int)run * R;
+    u16* yb = y + ((int64_t)b * T) * Cp + c;
+    if (c >= C) {  // operand padding channels
+      for (int r = 0; r < R && j0 + r < T; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, f32x2{0.f, 0.f});
+      continue;
+    }
+    const float* xb = x + ((int64_t)b * T) * C + c;
+    const f32x2 ear = f32x2{aexp[c], aexp[c + 1]} * INV_PI;
+    const f32x2 h = f32x2{ibeta[c], ibeta[c + 1]} * 0.5f;
+    if (j0 >= 6 && j0 + R + 6 <= T) {
+      f32x2 win[R + 12];
+#pragma unroll
+      for (int i = 0; i < R + 12; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(j0 - 6 + i) * C);
+      f32x2 o[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) o[r] = f32x2{0.f, 0.f};
+      // upsampled sample q (m = 2*j0 - 5 + q) feeds outputs r with 0 <= q - 2r <= 11 (down tap k = q - 2r,
+      // accumulated in ascending k as DownSample1d's conv does)
+#pragma unroll
+      for (int q = 0; q < 2 * R + 10; ++q) {
+        f32x2 u = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int k = 2 * kk + (q & 1);
+          u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
+        }
+        const f32x2 sv = snake2(u * 2.0f, ear, h);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int k = q - 2 * r;
+          if (k >= 0 && k < 12) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv, o[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
+    } else {
+      // sequence edges: replicate padding of the up (pad 5) and down (pad 5/6) filters
+      for (int j = j0; j < j0 + R && j < T; ++j) {
+        f32x2 o = f32x2{0.f, 0.f};
+        for (int k = 0; k < 12; ++k) {
+          int m = 2 * j + k - 5;
+          m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+          f32x2 u = f32x2{0.f, 0.f};
+          for (int kk = 0; kk < 6; ++kk) {
+            const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+            int xi = (m + 5 - ku) / 2;
+            xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+            u = fma2(f32x2{f.up[ku], f.up[ku]}, *reinterpret_cast<const f32x2*>(xb + (int64_t)xi * C), u);
+          }
+          o = fma2(f32x2{f.dn[k], f.dn[k]}, snake2(u * 2.0f, ear, h), o);
+        }
+        op_store2<PREC>(yb + (int64_t)j * Cp, y_lo, o);
+      }
+    }
+  }
+}
+
+int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                    const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                    hipStream_t s) {
+  if (!x || !y || !alpha_exp || !inv_beta || !up_filter || !down_filter || B <= 0 || T <= 0 || C <= 0)
+    return set_error(ALCM_E_INVALID, "activation1d_op: bad arguments");
+  if (Cp < C || Cp % 32) return set_error(ALCM_E_INVALID, "activation1d_op: Cp must be >= C and a multiple of 32");
+  if (C % 2) return set_error(ALCM_E_INVALID, "activation1d_op: C must be even");
+  if (prec < PREC_BF16 || prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "activation1d_op: bad prec");
+  if ((((uintptr_t)x) & 7) || (((uintptr_t)y) & 3)) return set_error(ALCM_E_INVALID, "activation1d_op: alignment");
+  const char* rs = std::getenv("ALCM_ACT_ROWS");  // diagnostics: rows per thread (8 or 16)
+  const int R = (rs && std::atoi(rs) == 16) ? 16 : 8;
+  const int runs = (T + R - 1) / R;
+  const int64_t total = (int64_t)B * runs * (Cp / 2);
+  if (total >= (1ll << 31) || (int64_t)B * T * Cp >= (1ll << 40))
+    return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
+  Taps12O f;
+  for (int k = 0; k < 12; ++k) {
+    f.up[k] = up_filter[k];
+    f.dn[k] = down_filter[k];
+  }
+  const int64_t y_lo = (int64_t)B * T * Cp;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
+  void* tok = prof_start(s);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
+                       (uint32_t)total, FastDiv((uint32_t)(Cp / 2)), FastDiv((uint32_t)runs));
+  };
+  if (R == 16) {
+    if (prec == PREC_SPLIT) launch(act_op_kernel<PREC_SPLIT, 16>);
+    else if (prec == PREC_BF16) launch(act_op_kernel<PREC_BF16, 16>);
+    else launch(act_op_kernel<PREC_F16, 16>);
+  } else {
+    if (prec == PREC_SPLIT) launch(act_op_kernel<PREC_SPLIT, 8>);
+    else if (prec == PREC_BF16) launch(act_op_kernel<PREC_BF16, 8>);
+    else launch(act_op_kernel<PREC_F16, 8>);
+  }
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::act_op_kernel<%d, %d>", prec == PREC_F16W2 ? PREC_F16 : prec, R);
+    const double e = (double)B * T;
+    prof_stop(tok, s, name, 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
+  }
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ implicit-GEMM conv on operand planes
+struct OpConvDev {
+  const u16* a;
+  int64_t a_lo;
+  int T, Cp, ksize, dil, pad;
+  const u16* w;
+  int64_t w_lo;
+  int kpad, N;
+  const float* bias;
+  const float* res;
+  float* out;
+  int out_act, accumulate;
+  float out_scale;
+  int tiles_per_batch;
+};
+
+constexpr int OC_AW = 48;       // window row stride (elements): conflict-free fragment reads from any start row
+constexpr int OC_HALO = 64;     // max (k-1)*dil
+
+__device__ __forceinline__ int oc_boff(int r, int kq) { return r * 32 + ((kq ^ ((r >> 2) & 2)) << 3); }
+
+// EPI: stage the output tile through LDS (over the dead window/weight buffers) and write whole
+// contiguous rows with 16-byte stores, residual prefetched at kernel start (narrow N, N % 4 == 0).
+template <int BM, int BN, int WGM, int WGN, int PREC, bool EPI>
+__global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
+  constexpr int TM = BM / (WGM * 16);
+  constexpr int TN = BN / (WGN * 16);
+  constexpr int NPA = PREC == PREC_SPLIT ? 2 : 1;
+  constexpr int NPB = (PREC == PREC_SPLIT || PREC == PREC_F16W2) ? 2 : 1;
+  constexpr int WRM = BM + OC_HALO;
+  constexpr int WCH = WRM * 4;  // 16-B chunks of one window plane
+  constexpr int WPER = (WCH + 255) / 256;
+  constexpr int BCH = BN * 4;
+  constexpr int BPER = (BCH + 255) / 256;
+  static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  constexpr int AW_BYTES = 2 * NPA * WRM * OC_AW * 2, BS_BYTES = 2 * NPB * BN * 32 * 2;
+  constexpr int OTS = BN + 4;  // output tile row stride (floats)
+  constexpr int OT_BYTES = EPI ? BM * OTS * 4 : 0;
+  constexpr int SMEM = AW_BYTES + BS_BYTES > OT_BYTES ? AW_BYTES + BS_BYTES : OT_BYTES;
+  constexpr int RPER = EPI ? (BM * BN / 4 + 255) / 256 : 1;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  auto Aw = reinterpret_cast<__bf16(*)[NPA][WRM * OC_AW]>(smem);
+  auto Bs = reinterpret_cast<__bf16(*)[NPB][BN * 32]>(smem + AW_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int b = blockIdx.x / P.tiles_per_batch;
+  const int t0 = (blockIdx.x - b * P.tiles_per_batch) * BM;
+  const int col0 = blockIdx.y * BN;
+  const int K = P.ksize;
+  const int WR = BM + (K - 1) * P.dil;
+  const int nC = P.Cp / 32;
+  const int nsteps = nC * K;
+
+  // EPI: this thread's residual float4s (tile rows are one contiguous block of mrows*N floats)
+  const int mrows = min(BM, P.T - t0);
+  const int64_t tile0 = ((int64_t)b * P.T + t0) * P.N;
+  float4 rp[RPER];
+  if constexpr (EPI) {
+    const int nq = mrows * (P.N / 4);
+#pragma unroll
+    for (int i = 0; i < RPER; ++i) {
+      const int e = tid + i * 256;
+      const int ec = e < nq ? e : 0;
+      rp[i] = P.res ? *reinterpret_cast<const float4*>(P.res + tile0 + (int64_t)ec * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  // Loads are issued unconditionally from clamped (always valid) addresses and out-of-range data is
+  // zeroed when it is written to LDS: divergent `if (ok) load` blocks make hipcc drain vmcnt(0) at
+  // every block boundary, which serialises the prefetch pipeline.
+  // window rows of this thread (fixed across chunks)
+  const u16* wsrc[WPER];
+  bool wok[WPER];
+#pragma unroll
+  for (int i = 0; i < WPER; ++i) {
+    const int c = tid + i * 256;
+    const int w = c >> 2;
+    const int ts = t0 + w - P.pad;
+    wok[i] = c < WCH && w < WR && ts >= 0 && ts < P.T;
+    const int tc = ts < 0 ? 0 : (ts >= P.T ? P.T - 1 : ts);
+    wsrc[i] = P.a + ((int64_t)b * P.T + tc) * P.Cp + (c & 3) * 8;
+  }
+  uint4 wv[WPER][NPA];
+  auto load_window = [&](int cc) {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i)
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) wv[i][p] = *reinterpret_cast<const uint4*>(wsrc[i] + cc * 32 + p * P.a_lo);
+  };
+  auto store_window = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int c = tid + i * 256;
+      if (WCH % 256 != 0 && c >= WCH) continue;
+      const uint32_t m = wok[i] ? 0xffffffffu : 0u;  // zero padding rows, branch-free
+#pragma unroll
+      for (int p = 0; p < NPA; ++p)
+        *reinterpret_cast<uint4*>(&Aw[buf][p][(c >> 2) * OC_AW + (c & 3) * 8]) =
+            make_uint4(wv[i][p].x & m, wv[i][p].y & m, wv[i][p].z & m, wv[i][p].w & m);
+    }
+  };
+
+  // weight rows of this thread
+  const u16* bsrc[BPER];
+  bool bok[BPER];
+#pragma unroll
+  for (int i = 0; i < BPER; ++i) {
+    const int c = tid + i * 256;
+    const int n = col0 + (c >> 2);
+    bok[i] = c < BCH && n < P.N;
+    bsrc[i] = P.w + (int64_t)(bok[i] ? n : 0) * P.kpad + (c & 3) * 8;
+  }
+  uint4 breg[2][BPER][NPB];
+  // K order: step s -> (chunk cc, tap), k0 = tap*Cp + cc*32; the loader walks it incrementally (no
+  // integer division per step); a load past the last step repeats the last tile (never stored/read)
+  int ld_tap = 0, ld_cc = 0;
+  auto load_b = [&](auto set_c) {
+    constexpr int set = decltype(set_c)::value;
+    const int k0 = ld_tap * P.Cp + ld_cc * 32;
+    if (ld_cc * K + ld_tap + 1 < nsteps) {
+      if (++ld_tap == K) {
+        ld_tap = 0;
+        ++ld_cc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPER; ++i)
+#pragma unroll
+      for (int p = 0; p < NPB; ++p) breg[set][i][p] = *reinterpret_cast<const uint4*>(bsrc[i] + k0 + p * P.w_lo);
+  };
+  auto store_b = [&](auto set_c, int buf) {
+    constexpr int set = decltype(set_c)::value;
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+      const int c = tid + i * 256;
+      if (BCH % 256 != 0 && c >= BCH) continue;
+      const int off = oc_boff(c >> 2, c & 3);
+      const uint32_t m = bok[i] ? 0xffffffffu : 0u;
+#pragma unroll
+      for (int p = 0; p < NPB; ++p) {
+        const uint4 v = breg[set][i][p];
+        *reinterpret_cast<uint4*>(&Bs[buf][p][off]) = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: window 0 and weight tile 0 in LDS, weight tile 1 in registers
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load_window(0);
+  load_b(S0{});
+  store_window(0);
+  store_b(S0{}, 0);
+  load_b(S1{});
+  __syncthreads();
+
+  const int a_base = (wm * TM * 16 + (lane & 15)) * OC_AW + (lane >> 4) * 8;
+  const int b_off = oc_boff(wn * TN * 16 + (lane & 15), lane >> 4);
+  // one K step s = cc*K + tap; SET (= s & 1) is compile-time so the register ring never lands in scratch.
+  // Every load is unconditional (clamped indices): conditional loads make hipcc drain vmcnt(0).
+  auto step = [&](int cc, int tap, int s, bool last_tap, auto set_c) {
+    constexpr int SET = decltype(set_c)::value;
+    load_b(set_c);  // tile s+2 (clamped) into register set SET, which held tile s (already in LDS)
+    const int a_off = a_base + tap * P.dil * OC_AW;
+    const int wb = cc & 1;
+    bf16x8 ah[TM], al[NPA == 2 ? TM : 1];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(&Aw[wb][0][a_off + i * 16 * OC_AW]);
+      if (NPA == 2) al[i] = *reinterpret_cast<const bf16x8*>(&Aw[wb][NPA - 1][a_off + i * 16 * OC_AW]);
+    }
+    bf16x8 bh[TN], bl[NPB == 2 ? TN : 1];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[SET][0][b_off + j * 16 * 32]);
+      if (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[SET][NPB - 1][b_off + j * 16 * 32]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (PREC == PREC_SPLIT) {
+          acc[i][j] = mfma16<PREC_BF16>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_BF16>(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_BF16>(ah[i], bh[j], acc[i][j]);
+        } else if constexpr (PREC == PREC_F16W2) {
+          acc[i][j] = mfma16<PREC_F16>(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_F16>(ah[i], bh[j], acc[i][j]);
+        } else {
+          acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
+        }
+      }
+    store_b(std::integral_constant<int, SET ^ 1>{}, SET ^ 1);  // tile s+1 (loaded during step s-1)
+    if (last_tap) store_window(wb ^ 1);
+    __syncthreads();
+  };
+  for (int cc = 0; cc < nC; ++cc) {
+    load_window(cc + 1 < nC ? cc + 1 : cc);  // next chunk's window (the last chunk reloads itself, unused)
+    const int s0 = cc * K;
+    const bool more = cc + 1 < nC;
+    int tap = 0;
+    if (s0 & 1) {
+      step(cc, 0, s0, more && K == 1, S1{});
+      tap = 1;
+    }
+    for (; tap + 1 < K; tap += 2) {
+      step(cc, tap, s0 + tap, false, S0{});
+      step(cc, tap + 1, s0 + tap + 1, more && tap + 2 == K, S1{});
+    }
+    if (tap < K) step(cc, tap, s0 + tap, more, S0{});
+  }
+
+  // epilogue
+  if constexpr (EPI) {
+    float* ot = reinterpret_cast<float*>(smem);  // the K loop's last barrier retired every LDS read
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = wn * TN * 16 + j * 16 + (lane & 15);
+          float v = acc[i][j][r];
+          if (P.bias && n < P.N) v += P.bias[n];
+          if (P.out_act) v = alcm_act(v, P.out_act);
+          ot[m * OTS + n] = v;
+        }
+      }
+    __syncthreads();
+    const int q4 = P.N / 4, nq = mrows * q4;
+    float* ob = P.out + tile0;
+#pragma unroll
+    for (int i = 0; i < RPER; ++i) {
+      const int e = tid + i * 256;
+      if (e >= nq) continue;
+      const int m = e / q4, n = (e - m * q4) * 4;
+      float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+      v.x += rp[i].x; v.y += rp[i].y; v.z += rp[i].z; v.w += rp[i].w;
+      v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+      if (P.accumulate) {
+        const float4 pv = *reinterpret_cast<const float4*>(ob + (int64_t)e * 4);
+        v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+      }
+      *reinterpret_cast<float4*>(ob + (int64_t)e * 4) = v;
+    }
+    return;
+  }
+  // direct stores: rows (b, t0 + m), channels-last output with row stride N
+  const int64_t obase = ((int64_t)b * P.T) * P.N;
+#pragma clang loop unroll(full)
+  for (int i = 0; i < TM; ++i) {
+#pragma clang loop unroll(full)
+    for (int r = 0; r < 4; ++r) {
+      const int t = t0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+      if (t >= P.T) continue;
+      const int64_t ro = obase + (int64_t)t * P.N;
+#pragma clang loop unroll(full)
+      for (int j = 0; j < TN; ++j) {
+        const int n = col0 + wn * TN * 16 + j * 16 + (lane & 15);
+        if (n >= P.N) continue;
+        float v = acc[i][j][r];
+        if (P.bias) v += P.bias[n];
+        if (P.out_act) v = alcm_act(v, P.out_act);
+        if (P.res) v += P.res[ro + n];
+        v *= P.out_scale;
+        if (P.accumulate) v += P.out[ro + n];
+        P.out[ro + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, bool EPI>
+static void launch_opconv_e(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
+  if (prec == PREC_SPLIT) hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, EPI>), grid, dim3(256), 0, s, Q);
+  else if (prec == PREC_F16) hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, EPI>), grid, dim3(256), 0, s, Q);
+  else if (prec == PREC_F16W2)
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, EPI>), grid, dim3(256), 0, s, Q);
+  else hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_BF16, EPI>), grid, dim3(256), 0, s, Q);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+static void launch_opconv(const OpConvDev& P, int B, int prec, double flops, double bytes, hipStream_t s) {
+  OpConvDev Q = P;
+  Q.tiles_per_batch = (P.T + BM - 1) / BM;
+  dim3 grid(B * Q.tiles_per_batch, (P.N + BN - 1) / BN);
+  // LDS-staged epilogue when one tile spans all N columns and rows are float4-aligned
+  const bool epi = BN <= 96 && P.N <= BN && P.N % 4 == 0;
+  void* tok = prof_start(s);
+  if (epi) launch_opconv_e<BM, BN, WGM, WGN, BN <= 96>(Q, grid, prec, s);
+  else launch_opconv_e<BM, BN, WGM, WGN, false>(Q, grid, prec, s);
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %s>", BM, BN, WGM, WGN, prec,
+                  epi ? "true" : "false");
+    prof_stop(tok, s, name, flops, bytes);
+  }
+}
+
+int opconv(const alcm_opconv_args& a, hipStream_t s) {
+  if (!a.a || !a.w || !a.out || a.B <= 0 || a.T <= 0 || a.N <= 0 || a.ksize <= 0 || a.dil <= 0)
+    return set_error(ALCM_E_INVALID, "opconv: bad arguments");
+  if (a.Cp <= 0 || a.Cp % 32) return set_error(ALCM_E_INVALID, "opconv: Cp must be a positive multiple of 32");
+  if ((a.ksize - 1) * a.dil > OC_HALO) return set_error(ALCM_E_INVALID, "opconv: receptive field too large");
+  if (2 * a.pad != (a.ksize - 1) * a.dil) return set_error(ALCM_E_INVALID, "opconv: only same-length convs");
+  if (a.kpad < a.ksize * a.Cp || a.kpad % 32) return set_error(ALCM_E_INVALID, "opconv: kpad mismatch");
+  if (a.prec < PREC_BF16 || a.prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "opconv: bad prec");
+  if ((((uintptr_t)a.a) & 15) || (((uintptr_t)a.w) & 15) || (a.a_lo_off % 8) || (a.w_lo_off % 8))
+    return set_error(ALCM_E_INVALID, "opconv: operands must be 16-byte aligned");
+  if (a.C <= 0 || a.C > a.Cp) return set_error(ALCM_E_INVALID, "opconv: C must be in (0, Cp]");
+  OpConvDev P{};
+  P.a = (const u16*)a.a; P.a_lo = a.a_lo_off;
+  P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
+  // planes of the packed weight: bf16 hi | bf16 lo | fp16 hi | fp16 lo, w_lo_off apart
+  const bool f16 = a.prec == PREC_F16 || a.prec == PREC_F16W2;
+  P.w = (const u16*)a.w + (f16 ? 2 * a.w_lo_off : 0);
+  P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.N = a.N;
+  P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_act = a.out_act; P.accumulate = a.accumulate;
+  P.out_scale = a.out_scale;
+  const double M = (double)a.B * a.T;
+  const int npa = a.prec == PREC_SPLIT ? 2 : 1, npb = (a.prec == PREC_SPLIT || a.prec == PREC_F16W2) ? 2 : 1;
+  const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;
+  const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
+                       M * a.N * 4.0 * (1 + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0));
+  const int N = a.N;
+  //                                               BM   BN  WGM WGN
+  if (N % 192 == 0 && N % 128 != 0) launch_opconv<128, 192, 2, 2>(P, a.B, a.prec, flops, bytes, s);
+  else if (N % 128 == 0) launch_opconv<128, 128, 2, 2>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 48) launch_opconv<128, 96, 2, 2>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 32) launch_opconv<256, 48, 4, 1>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 16) launch_opconv<256, 32, 4, 1>(P, a.B, a.prec, flops, bytes, s);
+  else launch_opconv<256, 16, 4, 1>(P, a.B, a.prec, flops, bytes, s);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace alcm
+
+extern "C" int alcm_activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                                    const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                                    alcm_stream_t stream) {
+  return alcm::activation1d_op(x, y, B, T, C, Cp, alpha_exp, inv_beta, up_filter, down_filter, prec,
+                               (hipStream_t)stream);
+}
+
+extern "C" int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream) {
+  if (!args) return alcm::set_error(ALCM_E_INVALID, "null args");
+  return alcm::opconv(*args, (hipStream_t)stream);
+}

@@ -28,15 +28,15 @@ def _round_up(x: int, m: int) -> int:
 def _prec(split: bool, prec: Optional[int]) -> int:
     """MFMA operand precision code: explicit `prec` (_hip.PREC_*) or split -> PREC_SPLIT / PREC_BF16."""
     if prec is not None:
-        assert prec in (_hip.PREC_BF16, _hip.PREC_SPLIT, _hip.PREC_F16), prec
+        assert prec in (_hip.PREC_BF16, _hip.PREC_SPLIT, _hip.PREC_F16, _hip.PREC_F16W2), prec
         return int(prec)
     return _hip.PREC_SPLIT if split else _hip.PREC_BF16
 
 
 @dataclass
 class PackedWeight:
-    """[rows][Kpad] GEMM operand planes bf16 hi, bf16 lo, fp16 (K index = tap*cpad + ci)."""
-    data: torch.Tensor  # int16 (3, rows, kpad) on device
+    """[rows][Kpad] GEMM operand planes bf16 hi, bf16 lo, fp16 hi, fp16 lo (K index = tap*cpad + ci)."""
+    data: torch.Tensor  # int16 (4, rows, kpad) on device
     rows: int
     cin: int
     cpad: int
@@ -62,7 +62,7 @@ def pack_conv_weight(w: torch.Tensor, transposed: bool = False, stride: int = 1,
         taps = k
     cpad = _round_up(cin, 8)
     kpad = _round_up(taps * cpad, BK)
-    out = torch.empty((3, cout, kpad), dtype=torch.int16, device=w.device)
+    out = torch.empty((4, cout, kpad), dtype=torch.int16, device=w.device)
     check(lib().alcm_pack_conv_weight(ptr(w), cout, cin, k, cpad, kpad, int(transposed), stride, phase, ptr(out),
                                       stream_handle()), "pack_conv_weight")
     return PackedWeight(out, cout, cin, cpad, taps, kpad)
@@ -314,7 +314,7 @@ def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], 
              act: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]] = None,
              residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
              accumulate_into: Optional[torch.Tensor] = None, split: bool = True,
-             prec: Optional[int] = None) -> torch.Tensor:
+             prec: Optional[int] = None, seg_tiles: int = 0) -> torch.Tensor:
     """Fused conv_{k,d}(Activation1d(x)) on channels-last (B, T, C) for C in {24, 48, 96}.
 
     act = (alpha, beta, up_filter, down_filter) of the SnakeBeta Activation1d (None: no activation)."""
@@ -338,5 +338,62 @@ def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], 
     out = accumulate_into if accumulate_into is not None else torch.empty((B, T, pw.rows), device=x_cl.device)
     a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
         out_scale, _prec(split, prec)
+    a.seg_tiles = seg_tiles
     check(lib().alcm_amp_conv(C.byref(a), stream_handle()), "amp_conv")
+    return out
+
+
+def operand_planes(x_cl: torch.Tensor, prec: int, Cp: Optional[int] = None) -> torch.Tensor:
+    """(B, T, C) fp32 -> MFMA operand planes int16 (NP, B, T, Cp) as alcm_activation1d_op writes them
+    (without the activation): fp16 for PREC_F16/F16W2, bf16 for PREC_BF16, bf16 hi/lo for PREC_SPLIT."""
+    B, T, Cc = x_cl.shape
+    Cp = Cp or _round_up(Cc, 32)
+    x = torch.nn.functional.pad(x_cl.float(), (0, Cp - Cc))
+    if prec in (_hip.PREC_F16, _hip.PREC_F16W2):
+        return x.half().view(torch.int16).unsqueeze(0).contiguous()
+    hi = x.bfloat16()
+    if prec == _hip.PREC_BF16:
+        return hi.view(torch.int16).unsqueeze(0).contiguous()
+    lo = (x - hi.float()).bfloat16()
+    return torch.stack([hi.view(torch.int16), lo.view(torch.int16)]).contiguous()
+
+
+def activation1d_op(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor, up_filter: torch.Tensor,
+                    down_filter: torch.Tensor, prec: int, Cp: Optional[int] = None) -> torch.Tensor:
+    """Activation1d of channels-last (B, T, C) into operand planes int16 (NP, B, T, Cp)."""
+    B, T, Cc = x_cl.shape
+    Cp = Cp or _round_up(Cc, 32)
+    x_cl = x_cl.contiguous()
+    ae, ib = snake_params(alpha, beta)
+    ae, ib = ae.contiguous(), ib.contiguous()
+    fu = up_filter.detach().reshape(-1).float().cpu().contiguous()
+    fd = down_filter.detach().reshape(-1).float().cpu().contiguous()
+    npl = 2 if prec == _hip.PREC_SPLIT else 1
+    y = torch.empty((npl, B, T, Cp), dtype=torch.int16, device=x_cl.device)
+    check(lib().alcm_activation1d_op(ptr(x_cl), ptr(y), B, T, Cc, Cp, ptr(ae), ptr(ib), fu.data_ptr(), fd.data_ptr(),
+                                     int(prec), stream_handle()), "activation1d_op")
+    return y
+
+
+def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
+           prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
+           accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None) -> torch.Tensor:
+    """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...)."""
+    npl, B, T, Cp = planes.shape
+    assert planes.dtype == torch.int16 and planes.is_contiguous()
+    N, cin, k = w.shape
+    assert cin == C_real <= Cp
+    if packed is None:
+        wp = torch.nn.functional.pad(w, (0, 0, 0, Cp - cin)).contiguous() if Cp != cin else w
+        packed = pack_conv_weight(wp)
+    a = _hip.OpConvArgs()
+    a.a, a.a_lo_off, a.B, a.T, a.C, a.Cp = ptr(planes), B * T * Cp, B, T, C_real, Cp
+    a.ksize, a.dil, a.pad = k, dilation, (k - 1) * dilation // 2
+    a.w, a.w_lo_off, a.kpad, a.N = ptr(packed.data), packed.lo_off, packed.kpad, N
+    a.bias = ptr(bias)
+    a.res = ptr(residual.contiguous()) if residual is not None else None
+    out = accumulate_into if accumulate_into is not None else torch.empty((B, T, N), device=planes.device)
+    a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
+        out_scale, int(prec)
+    check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
     return out

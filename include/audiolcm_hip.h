@@ -56,8 +56,9 @@ int alcm_check_device(int dev);
  * C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), MFMA with fp32 accumulate.  Operand precision `prec`:
  *   ALCM_PREC_BF16  (0) one v_mfma_f32_16x16x32_bf16 (operands rounded to bf16)
  *   ALCM_PREC_SPLIT (1) 3-term bf16 split (hi*hi + hi*lo + lo*hi): fp32-level accuracy, 3x the MFMA work
- *   ALCM_PREC_F16   (2) one v_mfma_f32_16x16x32_f16 (operands rounded to fp16) */
-enum { ALCM_PREC_BF16 = 0, ALCM_PREC_SPLIT = 1, ALCM_PREC_F16 = 2 };
+ *   ALCM_PREC_F16   (2) one v_mfma_f32_16x16x32_f16 (operands rounded to fp16)
+ *   ALCM_PREC_F16W2 (3) fp16 activation x fp16 hi+lo weight, 2 MFMAs (alcm_amp_conv only) */
+enum { ALCM_PREC_BF16 = 0, ALCM_PREC_SPLIT = 1, ALCM_PREC_F16 = 2, ALCM_PREC_F16W2 = 3 };
 enum { ALCM_OPND_ACT = 0, ALCM_OPND_ACT_T = 1, ALCM_OPND_WEIGHT = 2 };
 
 typedef struct alcm_operand {
@@ -67,8 +68,9 @@ typedef struct alcm_operand {
    *      t_src = t + tap*dil - pad (up == 2: nearest-x2 upsampled input, t_up = t + tap*dil - pad,
    *      t_src = t_up/2), zero outside [0, T_in) / ci >= C_in / k >= ksize*Cpad.
    * ACT_T: element (n, k) at ptr + k*st + n*sc, valid k < T_in, n < rows.
-   * WEIGHT: packed [rows][Kpad] planes: bf16 hi at ptr, bf16 lo at ptr + w_lo_off, fp16 at
- *         ptr + 2*w_lo_off (elements; w_lo_off = rows*Kpad as written by alcm_pack_conv_weight). */
+   * WEIGHT: packed [rows][Kpad] planes: bf16 hi at ptr, bf16 lo at ptr + w_lo_off, fp16 hi at
+ *         ptr + 2*w_lo_off, fp16 lo at ptr + 3*w_lo_off (elements; w_lo_off = rows*Kpad as written by
+ *         alcm_pack_conv_weight). */
   int64_t sb, st, sc;
   int T_in, C_in, Cpad, ksize, dil, pad, up;
   int rows_per_batch; /* ACT: rows m -> (b = m / rows_per_batch, t = m % rows_per_batch) */
@@ -109,9 +111,9 @@ typedef struct alcm_gemm_args {
 
 int alcm_gemm(const alcm_gemm_args* args, alcm_stream_t stream);
 
-/* pack a conv/linear weight W[co][ci][k] (fp32, DEVICE) into three [Cout][Kpad] planes (bf16 hi, bf16 lo,
- * fp16) with K index = tap*Cpad + ci. transposed=1 takes a ConvTranspose1d weight [ci][co][k] and a phase
- * (stride s, phase r) selecting taps j = r + s*(Q-1-tap), Q = k/s. out must hold 3*Cout*Kpad u16. */
+/* pack a conv/linear weight W[co][ci][k] (fp32, DEVICE) into four [Cout][Kpad] planes (bf16 hi, bf16 lo,
+ * fp16 hi, fp16 lo) with K index = tap*Cpad + ci. transposed=1 takes a ConvTranspose1d weight [ci][co][k]
+ * and a phase (stride s, phase r) selecting taps j = r + s*(Q-1-tap), Q = k/s. out must hold 4*Cout*Kpad u16. */
 int alcm_pack_conv_weight(const float* w, int c_out, int c_in, int k, int cpad, int kpad, int transposed,
                           int stride, int phase, void* out, alcm_stream_t stream);
 
@@ -152,9 +154,41 @@ typedef struct alcm_amp_args {
   float* out;
   int out_act, accumulate;
   float out_scale;
-  int prec; /* ALCM_PREC_* */
+  int prec;      /* ALCM_PREC_* */
+  int seg_tiles; /* 0: automatic; > 0 forces the output sub-tiles streamed per workgroup (tests) */
 } alcm_amp_args;
 int alcm_amp_conv(const alcm_amp_args* args, alcm_stream_t stream);
+
+/* ---------------------------------------------------------------- operand-format AMPBlock path
+ * (vocoder/bigvgan/models.py:72-81 as Activation1d -> conv, alcm_opconv.hip)
+ * alcm_activation1d_op: Activation1d of x (B,T,C) fp32 channels-last DEVICE into MFMA operand planes
+ *   y [B][T][Cp] of 2-byte elements (Cp = multiple of 32 >= C, channels >= C written as 0): prec
+ *   ALCM_PREC_F16 / F16W2 -> one fp16 plane; BF16 -> one bf16 plane; SPLIT -> bf16 hi plane at y and
+ *   bf16 lo plane at y + B*T*Cp.  alpha_exp / inv_beta DEVICE, filters HOST (12 taps). */
+int alcm_activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                         const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                         alcm_stream_t stream);
+/* alcm_opconv: out (B,T,N) = conv_{ksize,dil}(a) with same-length zero padding (2*pad == (ksize-1)*dil)
+ * on operand planes a (as written by alcm_activation1d_op, lo plane a_lo_off elements after hi), weights
+ * packed by alcm_pack_conv_weight with cpad = Cp; epilogue as alcm_gemm: v = acc + bias[n];
+ * v = act(v); v += res; v *= out_scale; if accumulate v += out.  prec: BF16 / SPLIT / F16 / F16W2
+ * (must match the planes a holds); C = real input channels (cost accounting). */
+typedef struct alcm_opconv_args {
+  const void* a;
+  int64_t a_lo_off;
+  int B, T, C, Cp;
+  int ksize, dil, pad;
+  const void* w;
+  int64_t w_lo_off;
+  int kpad, N;
+  const float* bias;
+  const float* res;
+  float* out;
+  int out_act, accumulate;
+  float out_scale;
+  int prec;
+} alcm_opconv_args;
+int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 
 /* ---------------------------------------------------------------- LCM scheduler pieces */
 /* coeffs (HOST array of 6): {sqrt_a, sqrt_b, c_out, c_skip, sqrt_a_prev, sqrt_b_prev};

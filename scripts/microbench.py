@@ -39,14 +39,13 @@ def bench_amp(B=32):
         for k, d in ((11, 5), (3, 1)):
             w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
             bias = torch.randn(C, device="cuda") * 0.05
-            for split in (True, False):
-                for act in (True, False):
-                    ms = timeit(lambda: K.amp_conv(x, w, bias, d, (k * d - d) // 2,
-                                                   act=(a, bt, f, f) if act else None, residual=r, split=split))
-                    gb = B * T * C * 4 * 3 / 1e9
-                    tf = 2 * B * T * C * C * k / 1e12
-                    print(f"amp C={C:3d} k={k:2d} d={d} split={int(split)} act={int(act)}: {ms:7.3f} ms "
-                          f"{gb / ms:6.2f} TB/s {tf / ms * 1e3:7.1f} TF/s")
+            for prec, act in ((1, True), (3, True), (2, True), (1, False)):
+                ms = timeit(lambda: K.amp_conv(x, w, bias, d, (k * d - d) // 2,
+                                               act=(a, bt, f, f) if act else None, residual=r, prec=prec))
+                gb = B * T * C * 4 * 3 / 1e9
+                tf = 2 * B * T * C * C * k / 1e12
+                print(f"amp C={C:3d} k={k:2d} d={d} prec={prec} act={int(act)}: {ms:7.3f} ms "
+                      f"{gb / ms:6.2f} TB/s {tf / ms * 1e3:7.1f} TF/s", flush=True)
 
 
 def bench_conv(B=32):
@@ -98,8 +97,74 @@ def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
     print(f"conv1 C={C} k={k}: {ms:.3f} ms {2 * B * T * C * C * k / 1e9 / ms:.1f} TF/s algorithmic")
 
 
+def bench_amp_ablate(B=32):
+    """phase costs of the fused narrow-stage kernel: ALCM_AMP_ABLATE bit0 = no activation, bit1 = no K loop,
+    bit2 = no epilogue (timing diagnostics; results are wrong under ablation)"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T in ((24, 159744), (48, 79872), (96, 39936)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        for k, d in ((11, 5), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            res = []
+            for ab in (0, 1, 2, 4, 3, 6, 5, 7):
+                os.environ["ALCM_AMP_ABLATE"] = str(ab)
+                res.append(timeit(lambda: K.amp_conv(x, w, None, d, (k * d - d) // 2, act=(a, bt, f, f), residual=r,
+                                                      split=True)))
+            os.environ.pop("ALCM_AMP_ABLATE")
+            print(f"amp C={C:3d} k={k:2d} split act res | full {res[0]:.3f} -act {res[1]:.3f} -mfma {res[2]:.3f} "
+                  f"-epi {res[3]:.3f} | only-epi {res[4]:.3f} only-act {res[5]:.3f} only-mfma {res[6]:.3f} "
+                  f"none {res[7]:.3f} ms", flush=True)
+
+
+def bench_op(B=32):
+    """operand-format path: act_op (Activation1d -> planes) and opconv per BigVGAN stage shape"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    stages = [(768, 2496, 2), (384, 9984, 2), (192, 19968, 2), (96, 39936, 3), (48, 79872, 3), (24, 159744, 3)]
+    for C, T, prec in stages:
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        for p in ((prec, 1) if prec != 1 else (1,)):
+            npl = 2 if p == 1 else 1
+            cp = (C + 31) // 32 * 32
+            gb = B * T * (C * 4 + cp * 2 * npl) / 1e9
+            for rows in ("8", "16"):
+                os.environ["ALCM_ACT_ROWS"] = rows
+                ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p))
+                print(f"act_op C={C:3d} prec={p} rows={rows}: {ms:7.3f} ms {gb / ms:6.2f} TB/s", flush=True)
+            pl = K.activation1d_op(x, a, bt, f, f, p)
+            for k, d in ((11, 5), (7, 3), (3, 1)):
+                w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+                wp = torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous()
+                pw = K.pack_conv_weight(wp)
+                ms = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
+                tf = 2 * B * T * C * C * k / 1e12
+                gb = B * T * (cp * 2 * npl + C * 8) / 1e9
+                mf = {1: 3, 3: 2}.get(p, 1)
+                print(f"  opconv C={C:3d} k={k:2d} d={d} prec={p}: {ms:7.3f} ms {tf / ms * 1e3:7.1f} TF/s alg "
+                      f"({tf * mf / ms * 1e3 / 2500:5.1%} MFMA) {gb / ms:5.2f} TB/s", flush=True)
+
+
+def bench_op1(B=32):
+    """one act_op + one opconv launch per tail/wide shape (target of rocprofv3 --pmc passes)"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T, prec, k, d in ((768, 2496, 2, 11, 5), (96, 39936, 3, 3, 1), (24, 159744, 3, 3, 1)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        cp = (C + 31) // 32 * 32
+        w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+        pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
+        for _ in range(2):
+            pl = K.activation1d_op(x, a, bt, f, f, prec)
+            K.opconv(pl, C, w, None, d, prec, residual=r, packed=pw)
+        torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["amp", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "conv": bench_conv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
+        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()

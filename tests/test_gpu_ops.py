@@ -16,7 +16,7 @@ SPLIT_TOL = 2e-5
 BF16_TOL = 1.5e-2
 F16_TOL = 2e-3
 PRECS = [1, 0, 2]                     # _hip.PREC_SPLIT, PREC_BF16, PREC_F16
-TOL = {1: SPLIT_TOL, 0: BF16_TOL, 2: F16_TOL}
+TOL = {1: SPLIT_TOL, 0: BF16_TOL, 2: F16_TOL, 3: F16_TOL}
 
 
 @pytest.fixture(scope="module")
@@ -179,11 +179,13 @@ def test_activation1d_long(K):
     np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=2e-5, atol=5e-6)
 
 
-@pytest.mark.parametrize("C,k,dil,T,act,res", [
-    (24, 11, 5, 700, True, True), (48, 7, 3, 333, True, False), (96, 3, 1, 150, True, True),
-    (96, 11, 1, 40, False, False), (24, 3, 1, 5, True, True)])
-@pytest.mark.parametrize("prec", PRECS)
-def test_amp_conv_fused(K, C, k, dil, T, act, res, prec):
+@pytest.mark.parametrize("C,k,dil,T,act,res,seg", [
+    (24, 11, 5, 700, True, True, 0), (48, 7, 3, 333, True, False, 0), (96, 3, 1, 150, True, True, 0),
+    (96, 11, 1, 40, False, False, 0), (24, 3, 1, 5, True, True, 0),
+    # several sub-tiles streamed through one workgroup's LDS ring (ring wrap-around, halo carry-over)
+    (96, 11, 5, 1000, True, True, 5), (48, 7, 3, 900, True, True, 4), (24, 11, 5, 2000, True, False, 3)])
+@pytest.mark.parametrize("prec", PRECS + [3])   # + PREC_F16W2 (fp16 activation x fp16 hi/lo weight)
+def test_amp_conv_fused(K, C, k, dil, T, act, res, seg, prec):
     """Fused Activation1d + conv (BigVGAN narrow stages) vs oracle Activation1d then F.conv1d (+ residual)."""
     from oracle import alcm_oracle as O
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
@@ -197,8 +199,22 @@ def test_amp_conv_fused(K, C, k, dil, T, act, res, prec):
     ref = F.conv1d(h, w, bias, dilation=dil, padding=(k * dil - dil) // 2) + (r if res else 0)
     y = K.amp_conv(dev(x.permute(0, 2, 1).contiguous()), dev(w), dev(bias), dil, (k * dil - dil) // 2,
                    act=(dev(a), dev(bt), f, f) if act else None,
-                   residual=dev(r.permute(0, 2, 1).contiguous()) if res else None, prec=prec).cpu().permute(0, 2, 1)
+                   residual=dev(r.permute(0, 2, 1).contiguous()) if res else None, prec=prec,
+                   seg_tiles=seg).cpu().permute(0, 2, 1)
     assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
+
+
+@pytest.mark.parametrize("C", [24, 48, 96])
+def test_amp_conv_streaming_is_tiling_invariant(K, C):
+    """The streamed ring (many sub-tiles per workgroup) matches one sub-tile per workgroup (up to the 1-ulp
+    differences of activation rows that fall on the replicate-padding edge path under one tiling only)."""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    x = dev(_r((3, 1500, C), 61, 1.2))
+    a, bt = dev(_r((C,), 62, 0.3)), dev(_r((C,), 63, 0.3))
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    w, bias = dev(_r((C, C, 11), 64, 0.7 / np.sqrt(C * 11))), dev(_r((C,), 65, 0.05))
+    ys = [K.amp_conv(x, w, bias, 5, 25, act=(a, bt, f, f), seg_tiles=s).cpu() for s in (1, 7, 1000)]
+    assert rel_l2(ys[1].numpy(), ys[0].numpy()) < 1e-6 and rel_l2(ys[2].numpy(), ys[0].numpy()) < 1e-6
 
 
 def test_amp_conv_post_tanh_and_accumulate(K):
@@ -249,3 +265,54 @@ def test_embeddings_golden(K):
     a = (w[:, None] * 1000.0 * gf[None]).double()
     np.testing.assert_allclose(ge.numpy(), torch.cat([torch.sin(a), torch.cos(a)], 1).numpy(), atol=2e-7)
     np.testing.assert_allclose(ge.numpy(), g["guidance_w4"], atol=3e-4)
+
+
+@pytest.mark.parametrize("C,T,k,dil", [(24, 300, 11, 5), (48, 200, 7, 3), (96, 257, 3, 1), (96, 130, 11, 5),
+                                       (192, 100, 3, 5), (384, 77, 7, 1), (768, 40, 11, 3), (64, 5, 3, 1)])
+@pytest.mark.parametrize("prec", [1, 0, 2, 3])
+def test_opconv(K, C, T, k, dil, prec):
+    """Implicit-GEMM conv on operand planes vs F.conv1d (planes built on the host from the same fp32 input)."""
+    B = 2
+    x = _r((B, T, C), 70)
+    w, bias = _r((C, C, k), 71, 0.7 / np.sqrt(C * k)), _r((C,), 72, 0.05)
+    r = _r((B, T, C), 73)
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1) + r
+    y = K.opconv(K.operand_planes(dev(x), prec), C, dev(w), dev(bias), dil, prec, residual=dev(r)).cpu()
+    assert y.shape == ref.shape
+    assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
+
+
+@pytest.mark.parametrize("prec", [1, 2, 3])
+def test_opconv_post_tanh_accumulate(K, prec):
+    """conv_post shape (N = 1, k7) with tanh, and the accumulate/out_scale epilogue (resblock mean)."""
+    x = _r((2, 333, 24), 74)
+    w, bias = _r((1, 24, 7), 75, 0.2), _r((1,), 76, 0.05)
+    ref = torch.tanh(F.conv1d(x.permute(0, 2, 1), w, bias, padding=3)).permute(0, 2, 1)
+    pl = K.operand_planes(dev(x), prec)
+    y = K.opconv(pl, 24, dev(w), dev(bias), 1, prec, out_act=4).cpu()
+    tol = 3e-5 if prec == 1 else TOL[prec]
+    assert rel_l2(y.numpy(), ref.numpy()) < tol
+    acc = dev(torch.ones((2, 333, 1)))
+    K.opconv(pl, 24, dev(w), dev(bias), 1, prec, out_act=4, out_scale=0.5, accumulate_into=acc)
+    assert rel_l2(acc.cpu().numpy(), (1 + 0.5 * ref).numpy()) < tol
+
+
+@pytest.mark.parametrize("C,T", [(24, 700), (96, 50), (768, 37), (48, 3), (192, 300), (24, 5000)])
+@pytest.mark.parametrize("prec", [1, 2])
+def test_activation1d_op(K, C, T, prec):
+    """Activation1d into operand planes == oracle Activation1d rounded to the operand format."""
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    x = _r((2, C, T), 77, 1.2)
+    a, bt = _r((C,), 78, 0.3), _r((C,), 79, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    ref = O.activation1d(x, a, bt, f, f).permute(0, 2, 1).contiguous()
+    pl = K.activation1d_op(dev(x.permute(0, 2, 1).contiguous()), dev(a), dev(bt), f, f, prec).cpu()
+    Cp = pl.shape[-1]
+    assert Cp % 32 == 0 and torch.all(pl[..., C:] == 0)
+    if prec == 2:
+        got = pl[0, ..., :C].view(torch.float16).float()
+        assert rel_l2(got.numpy(), ref.numpy()) < 1e-3
+    else:
+        got = pl[0, ..., :C].view(torch.bfloat16).float() + pl[1, ..., :C].view(torch.bfloat16).float()
+        assert rel_l2(got.numpy(), ref.numpy()) < 2e-5
