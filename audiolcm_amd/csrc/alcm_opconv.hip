@@ -217,9 +217,11 @@ constexpr int OC_HALO = 64;     // max (k-1)*dil
 
 __device__ __forceinline__ int oc_boff(int r, int kq) { return r * 32 + ((kq ^ ((r >> 2) & 2)) << 3); }
 
-// EPI: stage the output tile through LDS (over the dead window/weight buffers) and write whole
-// contiguous rows with 16-byte stores, residual prefetched at kernel start (narrow N, N % 4 == 0).
-template <int BM, int BN, int WGM, int WGN, int PREC, bool EPI>
+// TPS taps per K step (one LDS barrier per TPS*32-deep step); the output tile is staged through LDS
+// over the dead window/weight buffers, RG row groups (of TM*16 rows) at a time, and written as whole
+// BN-column row segments with 16-byte stores (residual read the same way).  VEC = N % 4 == 0.
+// PRE: prefetch the residual into registers at kernel start (narrow tiles whose tile fits one round).
+template <int BM, int BN, int WGM, int WGN, int PREC, int TPS, bool VEC>
 __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   constexpr int TM = BM / (WGM * 16);
   constexpr int TN = BN / (WGN * 16);
@@ -228,17 +230,22 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   constexpr int WRM = BM + OC_HALO;
   constexpr int WCH = WRM * 4;  // 16-B chunks of one window plane
   constexpr int WPER = (WCH + 255) / 256;
-  constexpr int BCH = BN * 4;
+  constexpr int BCH = BN * 4;   // 16-B chunks of one tap's weight tile (one plane)
   constexpr int BPER = (BCH + 255) / 256;
   static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "4 waves");
-  constexpr int AW_BYTES = 2 * NPA * WRM * OC_AW * 2, BS_BYTES = 2 * NPB * BN * 32 * 2;
-  constexpr int OTS = BN + 4;  // output tile row stride (floats)
-  constexpr int OT_BYTES = EPI ? BM * OTS * 4 : 0;
-  constexpr int SMEM = AW_BYTES + BS_BYTES > OT_BYTES ? AW_BYTES + BS_BYTES : OT_BYTES;
-  constexpr int RPER = EPI ? (BM * BN / 4 + 255) / 256 : 1;
+  static_assert(TPS == 1 || TPS == 2, "1 or 2 taps per step");
+  constexpr int AW_BYTES = 2 * NPA * WRM * OC_AW * 2, BS_BYTES = 2 * NPB * TPS * BN * 32 * 2;
+  constexpr int SMEM = AW_BYTES + BS_BYTES;
+  constexpr int OTS = BN + 4;                                   // output tile row stride (floats)
+  constexpr int GROUP_BYTES = TM * 16 * OTS * 4;                // one row group of the tile
+  constexpr int RG0 = SMEM / GROUP_BYTES;
+  constexpr int RG = RG0 >= WGM ? WGM : (RG0 >= 1 ? RG0 : 1);   // row groups per epilogue round
+  static_assert(GROUP_BYTES <= SMEM, "output row group must fit the LDS");
+  constexpr bool PRE = VEC && RG == WGM && (BM * BN / 4) <= 12 * 256;
+  constexpr int RPER = (BM * BN / 4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   auto Aw = reinterpret_cast<__bf16(*)[NPA][WRM * OC_AW]>(smem);
-  auto Bs = reinterpret_cast<__bf16(*)[NPB][BN * 32]>(smem + AW_BYTES);
+  auto Bs = reinterpret_cast<__bf16(*)[NPB][TPS][BN * 32]>(smem + AW_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -248,26 +255,27 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   const int K = P.ksize;
   const int WR = BM + (K - 1) * P.dil;
   const int nC = P.Cp / 32;
-  const int nsteps = nC * K;
-
-  // EPI: this thread's residual float4s (tile rows are one contiguous block of mrows*N floats)
+  const int SPC = (K + TPS - 1) / TPS;  // steps per chunk
+  const int nsteps = nC * SPC;
   const int mrows = min(BM, P.T - t0);
-  const int64_t tile0 = ((int64_t)b * P.T + t0) * P.N;
-  float4 rp[RPER];
-  if constexpr (EPI) {
+  const int64_t rowbase = (int64_t)b * P.T + t0;  // global output row of tile row 0
+
+  // residual prefetch (narrow tiles): tile rows are one contiguous block of mrows * N floats
+  float4 rp[RPER];  // dead (and eliminated) unless PRE
+  if constexpr (PRE) {
     const int nq = mrows * (P.N / 4);
 #pragma unroll
     for (int i = 0; i < RPER; ++i) {
       const int e = tid + i * 256;
       const int ec = e < nq ? e : 0;
-      rp[i] = P.res ? *reinterpret_cast<const float4*>(P.res + tile0 + (int64_t)ec * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rp[i] = P.res ? *reinterpret_cast<const float4*>(P.res + rowbase * P.N + (int64_t)ec * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 
   // Loads are issued unconditionally from clamped (always valid) addresses and out-of-range data is
   // zeroed when it is written to LDS: divergent `if (ok) load` blocks make hipcc drain vmcnt(0) at
   // every block boundary, which serialises the prefetch pipeline.
-  // window rows of this thread (fixed across chunks)
   const u16* wsrc[WPER];
   bool wok[WPER];
 #pragma unroll
@@ -309,38 +317,45 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
     bok[i] = c < BCH && n < P.N;
     bsrc[i] = P.w + (int64_t)(bok[i] ? n : 0) * P.kpad + (c & 3) * 8;
   }
-  uint4 breg[2][BPER][NPB];
-  // K order: step s -> (chunk cc, tap), k0 = tap*Cp + cc*32; the loader walks it incrementally (no
-  // integer division per step); a load past the last step repeats the last tile (never stored/read)
-  int ld_tap = 0, ld_cc = 0;
+  uint4 breg[2][TPS][BPER][NPB];
+  // step order: (chunk cc, tap group g) -> taps g*TPS + t (clamped to K-1: a missing tap of the last
+  // group is loaded but its MFMAs are skipped); the loader walks the order incrementally
+  int ld_g = 0, ld_cc = 0;
   auto load_b = [&](auto set_c) {
     constexpr int set = decltype(set_c)::value;
-    const int k0 = ld_tap * P.Cp + ld_cc * 32;
-    if (ld_cc * K + ld_tap + 1 < nsteps) {
-      if (++ld_tap == K) {
-        ld_tap = 0;
+#pragma unroll
+    for (int t = 0; t < TPS; ++t) {
+      const int tap = min(ld_g * TPS + t, K - 1);
+      const int k0 = tap * P.Cp + ld_cc * 32;
+#pragma unroll
+      for (int i = 0; i < BPER; ++i)
+#pragma unroll
+        for (int p = 0; p < NPB; ++p)
+          breg[set][t][i][p] = *reinterpret_cast<const uint4*>(bsrc[i] + k0 + p * P.w_lo);
+    }
+    if (ld_cc * SPC + ld_g + 1 < nsteps) {
+      if (++ld_g == SPC) {
+        ld_g = 0;
         ++ld_cc;
       }
     }
-#pragma unroll
-    for (int i = 0; i < BPER; ++i)
-#pragma unroll
-      for (int p = 0; p < NPB; ++p) breg[set][i][p] = *reinterpret_cast<const uint4*>(bsrc[i] + k0 + p * P.w_lo);
   };
   auto store_b = [&](auto set_c, int buf) {
     constexpr int set = decltype(set_c)::value;
 #pragma unroll
-    for (int i = 0; i < BPER; ++i) {
-      const int c = tid + i * 256;
-      if (BCH % 256 != 0 && c >= BCH) continue;
-      const int off = oc_boff(c >> 2, c & 3);
-      const uint32_t m = bok[i] ? 0xffffffffu : 0u;
+    for (int t = 0; t < TPS; ++t)
 #pragma unroll
-      for (int p = 0; p < NPB; ++p) {
-        const uint4 v = breg[set][i][p];
-        *reinterpret_cast<uint4*>(&Bs[buf][p][off]) = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+      for (int i = 0; i < BPER; ++i) {
+        const int c = tid + i * 256;
+        if (BCH % 256 != 0 && c >= BCH) continue;
+        const int off = oc_boff(c >> 2, c & 3);
+        const uint32_t m = bok[i] ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int p = 0; p < NPB; ++p) {
+          const uint4 v = breg[set][t][i][p];
+          *reinterpret_cast<uint4*>(&Bs[buf][p][t][off]) = make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+        }
       }
-    }
   };
 
   f32x4 acc[TM][TN];
@@ -349,7 +364,7 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: window 0 and weight tile 0 in LDS, weight tile 1 in registers
+  // prologue: window 0 and weight step 0 in LDS, weight step 1 in registers
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   load_window(0);
@@ -361,13 +376,8 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
 
   const int a_base = (wm * TM * 16 + (lane & 15)) * OC_AW + (lane >> 4) * 8;
   const int b_off = oc_boff(wn * TN * 16 + (lane & 15), lane >> 4);
-  // one K step s = cc*K + tap; SET (= s & 1) is compile-time so the register ring never lands in scratch.
-  // Every load is unconditional (clamped indices): conditional loads make hipcc drain vmcnt(0).
-  auto step = [&](int cc, int tap, int s, bool last_tap, auto set_c) {
-    constexpr int SET = decltype(set_c)::value;
-    load_b(set_c);  // tile s+2 (clamped) into register set SET, which held tile s (already in LDS)
+  auto mma_tap = [&](int wb, int tap, const __bf16* bh_base, const __bf16* bl_base) {
     const int a_off = a_base + tap * P.dil * OC_AW;
-    const int wb = cc & 1;
     bf16x8 ah[TM], al[NPA == 2 ? TM : 1];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -377,8 +387,8 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
     bf16x8 bh[TN], bl[NPB == 2 ? TN : 1];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      bh[j] = *reinterpret_cast<const bf16x8*>(&Bs[SET][0][b_off + j * 16 * 32]);
-      if (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(&Bs[SET][NPB - 1][b_off + j * 16 * 32]);
+      bh[j] = *reinterpret_cast<const bf16x8*>(bh_base + b_off + j * 16 * 32);
+      if (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bl_base + b_off + j * 16 * 32);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -395,71 +405,95 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
           acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
         }
       }
-    store_b(std::integral_constant<int, SET ^ 1>{}, SET ^ 1);  // tile s+1 (loaded during step s-1)
-    if (last_tap) store_window(wb ^ 1);
+  };
+  // one K step = tap group g of chunk cc; SET (= step parity) is compile-time so the register ring
+  // never lands in scratch
+  auto step = [&](int cc, int g, bool last_in_chunk, auto set_c) {
+    constexpr int SET = decltype(set_c)::value;
+    load_b(set_c);  // step s+2 (clamped) into register set SET, which held step s (already in LDS)
+    const int wb = cc & 1;
+    mma_tap(wb, g * TPS, &Bs[SET][0][0][0], &Bs[SET][NPB - 1][0][0]);
+    if (TPS == 2 && g * TPS + 1 < K) mma_tap(wb, g * TPS + 1, &Bs[SET][0][1][0], &Bs[SET][NPB - 1][1][0]);
+    store_b(std::integral_constant<int, SET ^ 1>{}, SET ^ 1);  // step s+1 (loaded during step s-1)
+    if (last_in_chunk) store_window(wb ^ 1);
     __syncthreads();
   };
   for (int cc = 0; cc < nC; ++cc) {
     load_window(cc + 1 < nC ? cc + 1 : cc);  // next chunk's window (the last chunk reloads itself, unused)
-    const int s0 = cc * K;
+    const int s0 = cc * SPC;
     const bool more = cc + 1 < nC;
-    int tap = 0;
+    int g = 0;
     if (s0 & 1) {
-      step(cc, 0, s0, more && K == 1, S1{});
-      tap = 1;
+      step(cc, 0, more && SPC == 1, S1{});
+      g = 1;
     }
-    for (; tap + 1 < K; tap += 2) {
-      step(cc, tap, s0 + tap, false, S0{});
-      step(cc, tap + 1, s0 + tap + 1, more && tap + 2 == K, S1{});
+    for (; g + 1 < SPC; g += 2) {
+      step(cc, g, false, S0{});
+      step(cc, g + 1, more && g + 2 == SPC, S1{});
     }
-    if (tap < K) step(cc, tap, s0 + tap, more, S0{});
+    if (g < SPC) step(cc, g, more, S0{});
   }
 
   // epilogue
-  if constexpr (EPI) {
+  if constexpr (VEC) {
     float* ot = reinterpret_cast<float*>(smem);  // the K loop's last barrier retired every LDS read
+    for (int h0 = 0; h0 < WGM; h0 += RG) {
+      if (wm >= h0 && wm < h0 + RG) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+          for (int r = 0; r < 4; ++r) {
+            const int m = (wm - h0) * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = wn * TN * 16 + j * 16 + (lane & 15);
-          float v = acc[i][j][r];
-          if (P.bias && n < P.N) v += P.bias[n];
-          if (P.out_act) v = alcm_act(v, P.out_act);
-          ot[m * OTS + n] = v;
+            for (int j = 0; j < TN; ++j) {
+              const int n = wn * TN * 16 + j * 16 + (lane & 15);
+              float v = acc[i][j][r];
+              if (P.bias && col0 + n < P.N) v += P.bias[col0 + n];
+              if (P.out_act) v = alcm_act(v, P.out_act);
+              ot[m * OTS + n] = v;
+            }
+          }
+      }
+      __syncthreads();
+      const int r0 = h0 * TM * 16;  // first tile row of this round
+      const int rows = min(RG * TM * 16, mrows - r0);
+      const int cq = min(BN, P.N - col0) / 4;  // float4 columns of this tile (N % 4 == 0)
+      const int nq = rows * cq;
+      for (int e = tid; e < (rows > 0 ? nq : 0); e += 256) {
+        const int m = e / cq, n = (e - m * cq) * 4;
+        const int64_t go = (rowbase + r0 + m) * P.N + col0 + n;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (PRE && P.N <= BN) {
+          // the tile spans all N columns: its rows are one contiguous block and e is the same element
+          // index the residual prefetch used
+          const int i = (e - tid) / 256;
+#pragma unroll
+          for (int ii = 0; ii < RPER; ++ii)
+            if (ii == i) rv = rp[ii];
+        } else if (P.res) {
+          rv = *reinterpret_cast<const float4*>(P.res + go);
         }
+        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+        v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+        if (P.accumulate) {
+          const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+          v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+        }
+        *reinterpret_cast<float4*>(P.out + go) = v;
       }
-    __syncthreads();
-    const int q4 = P.N / 4, nq = mrows * q4;
-    float* ob = P.out + tile0;
-#pragma unroll
-    for (int i = 0; i < RPER; ++i) {
-      const int e = tid + i * 256;
-      if (e >= nq) continue;
-      const int m = e / q4, n = (e - m * q4) * 4;
-      float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-      v.x += rp[i].x; v.y += rp[i].y; v.z += rp[i].z; v.w += rp[i].w;
-      v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
-      if (P.accumulate) {
-        const float4 pv = *reinterpret_cast<const float4*>(ob + (int64_t)e * 4);
-        v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
-      }
-      *reinterpret_cast<float4*>(ob + (int64_t)e * 4) = v;
+      __syncthreads();
     }
     return;
   }
-  // direct stores: rows (b, t0 + m), channels-last output with row stride N
-  const int64_t obase = ((int64_t)b * P.T) * P.N;
+  // direct stores (N % 4 != 0, e.g. conv_post): rows (b, t0 + m), channels-last output, row stride N
 #pragma clang loop unroll(full)
   for (int i = 0; i < TM; ++i) {
 #pragma clang loop unroll(full)
     for (int r = 0; r < 4; ++r) {
       const int t = t0 + wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
       if (t >= P.T) continue;
-      const int64_t ro = obase + (int64_t)t * P.N;
+      const int64_t ro = ((int64_t)b * P.T + t) * P.N;
 #pragma clang loop unroll(full)
       for (int j = 0; j < TN; ++j) {
         const int n = col0 + wn * TN * 16 + j * 16 + (lane & 15);
@@ -476,29 +510,33 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, bool EPI>
-static void launch_opconv_e(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
-  if (prec == PREC_SPLIT) hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, EPI>), grid, dim3(256), 0, s, Q);
-  else if (prec == PREC_F16) hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, EPI>), grid, dim3(256), 0, s, Q);
+template <int BM, int BN, int WGM, int WGN, int TPS, bool VEC>
+static void launch_opconv_v(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
+  constexpr int TPS_SPLIT = BN >= 192 ? 1 : TPS;  // LDS: the split operands double both buffers
+  if (prec == PREC_SPLIT)
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC>), grid, dim3(256), 0, s, Q);
+  else if (prec == PREC_F16)
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, TPS, VEC>), grid, dim3(256), 0, s, Q);
   else if (prec == PREC_F16W2)
-    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, EPI>), grid, dim3(256), 0, s, Q);
-  else hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_BF16, EPI>), grid, dim3(256), 0, s, Q);
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, TPS, VEC>), grid, dim3(256), 0, s, Q);
+  else hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_BF16, TPS, VEC>), grid, dim3(256), 0, s, Q);
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int TPS>
 static void launch_opconv(const OpConvDev& P, int B, int prec, double flops, double bytes, hipStream_t s) {
   OpConvDev Q = P;
   Q.tiles_per_batch = (P.T + BM - 1) / BM;
   dim3 grid(B * Q.tiles_per_batch, (P.N + BN - 1) / BN);
-  // LDS-staged epilogue when one tile spans all N columns and rows are float4-aligned
-  const bool epi = BN <= 96 && P.N <= BN && P.N % 4 == 0;
+  // LDS-staged epilogue for narrow layers (one tile spans N); wide layers store straight from the
+  // accumulators (measured faster there: the LDS round trip costs more than the coalescing saves)
+  const bool vec = P.N % 4 == 0 && P.N <= BN;
   void* tok = prof_start(s);
-  if (epi) launch_opconv_e<BM, BN, WGM, WGN, BN <= 96>(Q, grid, prec, s);
-  else launch_opconv_e<BM, BN, WGM, WGN, false>(Q, grid, prec, s);
+  if (vec) launch_opconv_v<BM, BN, WGM, WGN, TPS, true>(Q, grid, prec, s);
+  else launch_opconv_v<BM, BN, WGM, WGN, TPS, false>(Q, grid, prec, s);
   if (tok) {
-    char name[96];
-    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %s>", BM, BN, WGM, WGN, prec,
-                  epi ? "true" : "false");
+    char name[112];
+    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %d, %s>", BM, BN, WGM, WGN, prec, TPS,
+                  vec ? "true" : "false");
     prof_stop(tok, s, name, flops, bytes);
   }
 }
@@ -529,13 +567,14 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
                        M * a.N * 4.0 * (1 + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0));
   const int N = a.N;
-  //                                               BM   BN  WGM WGN
-  if (N % 192 == 0 && N % 128 != 0) launch_opconv<128, 192, 2, 2>(P, a.B, a.prec, flops, bytes, s);
-  else if (N % 128 == 0) launch_opconv<128, 128, 2, 2>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 48) launch_opconv<128, 96, 2, 2>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 32) launch_opconv<256, 48, 4, 1>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 16) launch_opconv<256, 32, 4, 1>(P, a.B, a.prec, flops, bytes, s);
-  else launch_opconv<256, 16, 4, 1>(P, a.B, a.prec, flops, bytes, s);
+  // one tap per K step (two taps per step measured slower: the larger weight buffers cost occupancy)
+  //                                               BM   BN  WGM WGN TPS
+  if (N % 192 == 0 && N % 128 != 0) launch_opconv<128, 192, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
+  else if (N % 128 == 0) launch_opconv<128, 128, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 48) launch_opconv<128, 96, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 32) launch_opconv<256, 48, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
+  else if (N > 16) launch_opconv<256, 32, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
+  else launch_opconv<256, 16, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
   ALCM_HIP(hipGetLastError());
   return 0;
 }
