@@ -164,8 +164,74 @@ def main_dit_vae():
                   flush=True)
 
 
+def run_dit_groups(policy, Wd, ctx, xT, noise):
+    """DiT sampler only (float64), operands rounded per group: 'ffn', 'qkv' (to_q/k/v), 'out' (to_out),
+    'proj' (TemporalTransformer proj_in/out 1x1), 'emb' (embedders, proj_in k5, final layer),
+    'attn' (QK^T and PV products)."""
+    real_conv, real_lin, real_einsum = F.conv1d, F.linear, torch.einsum
+
+    def grp_w(w):
+        if w.dim() == 3 and w.shape[-1] == 9:
+            return "ffn"
+        if w.dim() == 3 and w.shape[-1] == 1 and w.shape[0] == w.shape[1] == 576:
+            return "proj"
+        if w.dim() == 2 and w.shape == (576, 576):
+            return "qkv_or_out"
+        return "emb"
+
+    def conv1d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+        a_f, w_f = policy.get(grp_w(w), ("f32", "f32"))
+        return real_conv(rnd(x.to(w.dtype), a_f), rnd(w, w_f), b, stride, padding, dilation, groups)
+
+    def linear(x, w, b=None):
+        g = grp_w(w)
+        if g == "qkv_or_out":
+            g = "out" if b is not None else "qkv"
+        a_f, w_f = policy.get(g, ("f32", "f32"))
+        return real_lin(rnd(x.to(w.dtype), a_f), rnd(w, w_f), b)
+
+    def einsum(eq, a, b):
+        a_f, b_f = policy.get("attn", ("f32", "f32"))
+        return real_einsum(eq, rnd(a, a_f), rnd(b, b_f))
+
+    ns = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("_")})
+    ns.conv1d, ns.linear = conv1d, linear
+    tns = types.SimpleNamespace(**{k: getattr(torch, k) for k in dir(torch) if not k.startswith("__")})
+    tns.einsum = einsum
+    old_F, old_t = O.F, O.torch
+    O.F, O.torch = ns, tns
+    try:
+        eps_fn = lambda x, t, w: O.dit_forward(Wd, x, t, ctx, w)
+        return O.lcm_sample(eps_fn, ctx, xT, noise, 2, 5.0)
+    finally:
+        O.F, O.torch = old_F, old_t
+
+
+def main_dit_groups():
+    torch.set_num_threads(max(1, min(8, len(os.sched_getaffinity(0)))))
+    Wd = {k: v.double() for k, v in recipe.dit_state(0).items()}
+    g = np.load(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "e2e_S2_B2.npz"))
+    ctx = recipe.synthetic_context(2).double()
+    xT, noise = torch.from_numpy(g["x_T"]).double(), torch.from_numpy(g["noise"]).double()
+    with torch.no_grad():
+        z0 = run_dit_groups({}, Wd, ctx, xT, noise)
+        f16, a16 = ("f16", "f16"), ("f16", "f32")
+        cases = {"attn f16": {"attn": f16}, "attn bf16": {"attn": ("bf16", "bf16")},
+                 "qkv f16": {"qkv": f16}, "qkv act-f16": {"qkv": a16}, "out f16": {"out": f16},
+                 "out act-f16": {"out": a16}, "proj f16": {"proj": f16}, "proj act-f16": {"proj": a16},
+                 "emb f16": {"emb": f16}, "emb act-f16": {"emb": a16},
+                 "ffn+attn f16 + qkv/out/proj act-f16": {"ffn": f16, "attn": f16, "qkv": a16, "out": a16,
+                                                         "proj": a16}}
+        for name, pol in cases.items():
+            z = run_dit_groups(pol, Wd, ctx, xT, noise)
+            print(f"{name:40s} latent {float((z - z0).norm() / z0.norm()):.2e}", flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "ditvae":
         main_dit_vae()
+    elif len(sys.argv) > 1 and sys.argv[1] == "dit":
+        main_dit_groups()
     else:
         main()
+
