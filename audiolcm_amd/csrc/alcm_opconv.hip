@@ -566,6 +566,10 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;
   const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
                        M * a.N * 4.0 * (1 + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0));
+  if (wconv_try(a, P.w, flops, bytes, s)) {
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
   const int N = a.N;
   // one tap per K step (two taps per step measured slower: the larger weight buffers cost occupancy)
   //                                               BM   BN  WGM WGN TPS

@@ -147,6 +147,28 @@ def bench_op(B=32):
                       f"({tf * mf / ms * 1e3 / 2500:5.1%} MFMA) {gb / ms:5.2f} TB/s", flush=True)
 
 
+def bench_wconv(B=32):
+    """wide conv (alcm_wconv.hip) vs the 128-row opconv_kernel on the BigVGAN stage 0-2 shapes"""
+    for C, T in ((768, 2496), (384, 9984), (192, 19968)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        for p in (2, 0):
+            pl = K.operand_planes(x, p)
+            for k, d in ((11, 5), (7, 3), (3, 1)):
+                w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+                pw = K.pack_conv_weight(w)
+                tf = 2 * B * T * C * C * k / 1e12
+                outs, line = [], []
+                for wc in os.environ.get("WCONV_VARS", "0,1").split(","):
+                    os.environ["ALCM_WCONV"] = wc
+                    ms = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
+                    outs.append(K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
+                    line.append(f"wconv={wc} {ms:7.3f} ms {tf / ms * 1e3:7.1f} TF/s")
+                os.environ.pop("ALCM_WCONV")
+                diff = max(float((outs[0] - o).abs().max()) for o in outs[1:])
+                print(f"C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line) + f" | max|diff| {diff:.2e}", flush=True)
+
+
 def bench_op1(B=32):
     """one act_op + one opconv launch per tail/wide shape (target of rocprofv3 --pmc passes)"""
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
@@ -167,4 +189,4 @@ if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["amp", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
+        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()

@@ -282,6 +282,27 @@ def test_opconv(K, C, T, k, dil, prec):
     assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
 
 
+@pytest.mark.parametrize("C,T,k,dil", [(768, 600, 11, 5), (384, 1100, 7, 3), (192, 1500, 3, 1), (256, 700, 5, 2),
+                                       (384, 520, 11, 1)])
+@pytest.mark.parametrize("prec", [0, 2])
+def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
+    """Wide-layer kernel (alcm_wconv.hip: 256-row tiles, LDS-DMA staging) vs F.conv1d and vs the 128-row
+    opconv_kernel on the same operand planes (identical products, only the fp32 summation order differs)."""
+    B = 2
+    x = _r((B, T, C), 80)
+    w, bias = _r((C, C, k), 81, 0.7 / np.sqrt(C * k)), _r((C,), 82, 0.05)
+    r = _r((B, T, C), 83)
+    ref = (F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1) + r) * 0.5
+    pl = K.operand_planes(dev(x), prec)
+    acc = dev(torch.ones((B, T, C)))
+    y = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5, accumulate_into=acc).cpu() - 1
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+    monkeypatch.setenv("ALCM_WCONV", "0")
+    acc0 = dev(torch.ones((B, T, C)))
+    y0 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5, accumulate_into=acc0).cpu() - 1
+    assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("prec", [1, 2, 3])
 def test_opconv_post_tanh_accumulate(K, prec):
     """conv_post shape (N = 1, k7) with tanh, and the accumulate/out_scale epilogue (resblock mean)."""
