@@ -57,7 +57,9 @@ class OpConvArgs(C.Structure):
     _fields_ = [("a", vp), ("a_lo_off", i64), ("B", C.c_int), ("T", C.c_int), ("C", C.c_int), ("Cp", C.c_int),
                 ("ksize", C.c_int), ("dil", C.c_int), ("pad", C.c_int), ("w", vp), ("w_lo_off", i64),
                 ("kpad", C.c_int), ("N", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
-                ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int)]
+                ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int),
+                ("act_plane", vp), ("act_plane_lo_off", i64), ("act_alpha_exp", fp), ("act_inv_beta", fp),
+                ("act_up_filter", fp), ("act_down_filter", fp)]
 
 
 class NamedTensor(C.Structure):

@@ -1,0 +1,151 @@
+// Activation1d (alias_free_torch/act.py:23-27: UpSample1d x2 -> SnakeBeta -> DownSample1d) on values that
+// are already on chip, written as MFMA operand planes.  Shared by the standalone act_op_kernel and the
+// fused conv epilogues (alcm_opconv.hip, alcm_wconv.hip), which apply it to an LDS-staged fp32 conv tile
+// so the conv output never makes an fp32 round trip through HBM before the next conv reads it.
+#pragma once
+#include "alcm_common.h"
+
+namespace alcm {
+
+struct Taps12O {
+  float up[12], dn[12];
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// x + h - h*cos(2*pi*r), r = x*ea_rev - rint(x*ea_rev): SnakeBeta (activations.py:62-119) with
+// h = inv_beta/2, ea_rev = exp(alpha)/pi, since sin^2(z) = 1/2 - cos(2z)/2
+__device__ __forceinline__ f32x2 snake2(f32x2 u, f32x2 ear, f32x2 h) {
+  const f32x2 z = u * ear;
+  f32x2 r;
+  r.x = z.x - rintf(z.x);
+  r.y = z.y - rintf(z.y);
+  f32x2 c;
+  c.x = __builtin_amdgcn_cosf(r.x);
+  c.y = __builtin_amdgcn_cosf(r.y);
+  return fma2(-h, c, u + h);
+}
+
+// two adjacent channels -> operand plane(s): fp16 (F16/F16W2), bf16 (BF16), bf16 hi at hi + bf16 lo at
+// hi + lo_off (SPLIT)
+template <int PREC>
+__device__ __forceinline__ void op_store2(u16* hi, int64_t lo_off, f32x2 v) {
+  uint32_t wh, wl = 0;
+  if constexpr (PREC == PREC_F16 || PREC == PREC_F16W2) {
+    wh = (uint32_t)__builtin_bit_cast(u16, (_Float16)v.x) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)v.y) << 16);
+  } else {
+    const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+    wh = (uint32_t)__builtin_bit_cast(u16, hx) | ((uint32_t)__builtin_bit_cast(u16, hy) << 16);
+    if (PREC == PREC_SPLIT)
+      wl = (uint32_t)__builtin_bit_cast(u16, (__bf16)(v.x - (float)hx)) |
+           ((uint32_t)__builtin_bit_cast(u16, (__bf16)(v.y - (float)hy)) << 16);
+  }
+  *reinterpret_cast<uint32_t*>(hi) = wh;
+  if (PREC == PREC_SPLIT) *reinterpret_cast<uint32_t*>(hi + lo_off) = wl;
+}
+
+// Activation1d of R consecutive outputs j0 .. j0+R-1 of a channel pair whose input rows j0-6 .. j0+R+5 are
+// all inside the sequence: win[i] = x[j0 - 6 + i].  Upsampled sample q (m = 2*j0 - 5 + q) feeds outputs r
+// with 0 <= q - 2r <= 11 (down tap k = q - 2r, accumulated in ascending k as DownSample1d's conv does).
+template <int R>
+__device__ __forceinline__ void act_run_interior(const f32x2 (&win)[R + 12], const Taps12O& f, f32x2 ear, f32x2 h,
+                                                 f32x2 (&o)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) o[r] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 2 * R + 10; ++q) {
+    f32x2 u = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int k = 2 * kk + (q & 1);
+      u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
+    }
+    const f32x2 sv = snake2(u * 2.0f, ear, h);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = q - 2 * r;
+      if (k >= 0 && k < 12) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv, o[r]);
+    }
+  }
+}
+
+// One output j anywhere in [0, T): replicate padding of the up filter's input (pad 5) and of the down
+// filter's input (pad 5 / 6) as index clamps.  ld(i) returns input row i (0 <= i < T) of the pair.
+template <typename LD>
+__device__ __forceinline__ f32x2 act_one_clamped(int j, int T, const Taps12O& f, f32x2 ear, f32x2 h, LD ld) {
+  f32x2 o = f32x2{0.f, 0.f};
+  for (int k = 0; k < 12; ++k) {
+    int m = 2 * j + k - 5;
+    m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+    f32x2 u = f32x2{0.f, 0.f};
+    for (int kk = 0; kk < 6; ++kk) {
+      const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+      int xi = (m + 5 - ku) / 2;
+      xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+      u = fma2(f32x2{f.up[ku], f.up[ku]}, ld(xi), u);
+    }
+    o = fma2(f32x2{f.dn[k], f.dn[k]}, snake2(u * 2.0f, ear, h), o);
+  }
+  return o;
+}
+
+// Fused-epilogue parameters: Activation1d of the conv output into operand planes [B][T][Cp]
+struct ActEpiDev {
+  u16* plane;
+  int64_t plane_lo;  // SPLIT: elements from the hi plane to the lo plane
+  int Cp;            // plane channel stride (channels C .. Cp-1 are written as zeros)
+  const float* aexp;
+  const float* ibeta;
+  Taps12O f;
+};
+
+constexpr int ACT_EPI_R = 8;  // output rows per work item
+constexpr int ACT_EPI_HALO = 8;  // conv tile rows computed beyond each side of the emitted rows
+
+// Activation1d of an LDS-staged fp32 tile.  tile[(t - trow0) * ots + col] holds v(b, t, c0 + col) for
+// t in [trow0, trow0 + rows) (clamped to [0, T)); emits rows [e_lo, e_hi) for columns [0, ncol) (ncol even)
+// of batch b into the planes; channels c >= C are written as zeros (operand padding).  The tile must cover
+// [max(e_lo - 6, 0), min(e_hi + 6, T)).
+template <int PREC>
+__device__ __forceinline__ void act_epilogue_tile(const float* tile, int ots, int trow0, int e_lo, int e_hi, int T,
+                                                  int ncol, int c0, int C, int b, const ActEpiDev& A, int tid,
+                                                  int nthr) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int R = ACT_EPI_R;
+  const int npairs = ncol >> 1;
+  const int nrun = (e_hi - e_lo + R - 1) / R;
+  for (int w = tid; w < npairs * nrun; w += nthr) {
+    const int run = w / npairs, p = w - run * npairs;
+    const int c = c0 + 2 * p;
+    const int j0 = e_lo + run * R;
+    const int jn = min(R, e_hi - j0);
+    u16* yb = A.plane + ((int64_t)b * T) * A.Cp + c;
+    if (c >= C) {
+      for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, f32x2{0.f, 0.f});
+      continue;
+    }
+    const float* col = tile + 2 * p;
+    const f32x2 ear = f32x2{A.aexp[c], A.aexp[c + 1]} * INV_PI;
+    const f32x2 h = f32x2{A.ibeta[c], A.ibeta[c + 1]} * 0.5f;
+    if (jn == R && j0 >= 6 && j0 + R + 6 <= T) {
+      f32x2 win[R + 12];
+#pragma unroll
+      for (int i = 0; i < R + 12; ++i) win[i] = *reinterpret_cast<const f32x2*>(col + (j0 - 6 + i - trow0) * ots);
+      f32x2 o[R];
+      act_run_interior<R>(win, A.f, ear, h, o);
+#pragma unroll
+      for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o[r]);
+    } else {
+      for (int r = 0; r < jn; ++r) {
+        const f32x2 o = act_one_clamped(j0 + r, T, A.f, ear, h, [&](int i) {
+          return *reinterpret_cast<const f32x2*>(col + (i - trow0) * ots);
+        });
+        op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o);
+      }
+    }
+  }
+}
+
+}  // namespace alcm

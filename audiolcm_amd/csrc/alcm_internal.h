@@ -44,7 +44,11 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
-int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, double flops, double bytes, hipStream_t s);
+// whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
+bool opconv_act_supported(int prec, int N, int Cp_in);
+// actepi: const ActEpiDev* (alcm_actepi.h) or nullptr
+int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
+              hipStream_t s);
 
 bool prof_enabled();
 void* prof_start(hipStream_t s);

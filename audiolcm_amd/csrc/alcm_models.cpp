@@ -859,8 +859,8 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
 
 // ------------------------------------------------------------------ BigVGAN
 struct VocWs {
-  float *x, *y, *rb, *a, *t;
-  u16* pl;  // Activation1d output as MFMA operand planes (2 planes of B * T * Cp)
+  float *x, *y, *rb, *t;
+  u16 *pl, *pl2;  // Activation1d outputs as MFMA operand planes (each 2 planes of B * T * Cp)
   int64_t pl_lo;
 };
 static size_t voc_elems(const VocW& G, int M) {
@@ -884,9 +884,9 @@ static VocWs plan_voc(const VocW& G, Bump& bp, int B, int M) {
   w.x = bp.take<float>(e);
   w.y = bp.take<float>(e);
   w.rb = bp.take<float>(e);
-  w.a = bp.take<float>(e);
   w.t = bp.take<float>(e);
   w.pl = bp.take<u16>(2 * pe);
+  w.pl2 = bp.take<u16>(2 * pe);
   w.pl_lo = (int64_t)pe;
   return w;
 }
@@ -905,11 +905,22 @@ static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs&
   return activation1d_op(x, w.pl, B, T, C, round_up(C, 32), a.aexp, a.ibeta, a.fup, a.fdn, prec, s);
 }
 
+// conv on the operand planes `in`; with `act` the epilogue also writes Activation1d(conv + bias (+ res)) into
+// the planes `act_out` (alcm_actepi.h), and `out` may be null
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
-                      float* out, float out_scale, int accumulate, int out_act, int prec) {
+                      float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
+                      const ActW* act = nullptr, u16* act_out = nullptr) {
   alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
-  g.a = w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
+  g.a = in ? in : w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
+  if (act) {
+    g.act_plane = act_out;
+    g.act_plane_lo_off = (int64_t)B * T * round_up(cw.w.rows, 32);
+    g.act_alpha_exp = act->aexp;
+    g.act_inv_beta = act->ibeta;
+    g.act_up_filter = act->fup;
+    g.act_down_filter = act->fdn;
+  }
   g.B = B; g.T = T; g.C = cw.w.cin; g.Cp = cw.w.cpad;
   g.ksize = cw.w.taps; g.dil = dil; g.pad = (cw.w.taps - 1) * dil / 2;
   g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
@@ -952,13 +963,31 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
                     Out{u, (int64_t)To * S.cout, S.cout, 1, S.rate, S.off[r]}, o));
     }
     // x = mean over k in (3,7,11) of AMPBlock1(k, (1,3,5))(u)  (models.py:190-199, 72-81); each half-layer
-    // is Activation1d -> operand planes (alcm_opconv.hip act_op) -> implicit-GEMM conv on the planes
+    // is Activation1d -> operand planes -> implicit-GEMM conv on the planes.  Fused form (every stage the
+    // kernels support at this precision): the first Activation1d of a resblock runs standalone (act_op); every
+    // later one runs in the epilogue of the conv that produces its input (conv1 writes only planes; conv2
+    // writes the fp32 running state, ping-ponged between rb and y since its tiles overlap, plus planes)
     const float inv = 1.0f / (float)S.rb.size();
+    const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
       const float* cur = u;
+      float* nxt = rb;
       for (size_t l = 0; l < A.dil.size(); ++l) {
         const bool last = l + 1 == A.dil.size();
+        if (fuse) {
+          if (l == 0) ALCM_TRY(act_planes(s, A.act[0], cur, w, B, To, S.cout, pamp));
+          ALCM_TRY(plane_conv(s, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, w.pl,
+                              &A.act[2 * l + 1], w.pl2));
+          if (last) {
+            ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, x, inv, j > 0, 0, pamp, w.pl2));
+          } else {
+            ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, nxt, 1.f, 0, 0, pamp, w.pl2, &A.act[2 * l + 2], w.pl));
+            cur = nxt;
+            nxt = nxt == rb ? y : rb;
+          }
+          continue;
+        }
         ALCM_TRY(act_planes(s, A.act[2 * l], cur, w, B, To, S.cout, pamp));
         ALCM_TRY(plane_conv(s, A.c1[l], w, B, To, A.dil[l], nullptr, y, 1.f, 0, 0, pamp));
         ALCM_TRY(act_planes(s, A.act[2 * l + 1], y, w, B, To, S.cout, pamp));

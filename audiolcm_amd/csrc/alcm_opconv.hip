@@ -19,12 +19,9 @@
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
+#include "alcm_actepi.h"
 
 namespace alcm {
-
-struct Taps12O {
-  float up[12], dn[12];
-};
 
 // sin(x)^2: Cody-Waite quadrant reduction + minimax sin/cos on |r| <= pi/4 (~1 ulp, branch-free)
 __device__ __forceinline__ float op_sin_sq(float x) {
@@ -47,37 +44,6 @@ __device__ __forceinline__ float op_sin_sq(float x) {
 // 1/2 - cos(2z)/2 with 2z reduced to [-1/2, 1/2] revolutions and the hardware v_cos_f32 (a handful of
 // instructions instead of a ~20-op polynomial).  Pairs at or beyond C write zeros (operand padding).
 constexpr int AOP_R = 16;  // output rows per thread
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-// x + h - h*cos(2*pi*r), r = x*ea_rev - rint(x*ea_rev): SnakeBeta with h = inv_beta/2, ea_rev = exp(alpha)/pi
-__device__ __forceinline__ f32x2 snake2(f32x2 u, f32x2 ear, f32x2 h) {
-  const f32x2 z = u * ear;
-  f32x2 r;
-  r.x = z.x - rintf(z.x);
-  r.y = z.y - rintf(z.y);
-  f32x2 c;
-  c.x = __builtin_amdgcn_cosf(r.x);
-  c.y = __builtin_amdgcn_cosf(r.y);
-  return fma2(-h, c, u + h);
-}
-
-template <int PREC>
-__device__ __forceinline__ void op_store2(u16* hi, int64_t lo_off, f32x2 v) {
-  uint32_t wh, wl = 0;
-  if constexpr (PREC == PREC_F16 || PREC == PREC_F16W2) {
-    wh = (uint32_t)__builtin_bit_cast(u16, (_Float16)v.x) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)v.y) << 16);
-  } else {
-    const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
-    wh = (uint32_t)__builtin_bit_cast(u16, hx) | ((uint32_t)__builtin_bit_cast(u16, hy) << 16);
-    if (PREC == PREC_SPLIT)
-      wl = (uint32_t)__builtin_bit_cast(u16, (__bf16)(v.x - (float)hx)) |
-           ((uint32_t)__builtin_bit_cast(u16, (__bf16)(v.y - (float)hy)) << 16);
-  }
-  *reinterpret_cast<uint32_t*>(hi) = wh;
-  if (PREC == PREC_SPLIT) *reinterpret_cast<uint32_t*>(hi + lo_off) = wl;
-}
 
 // thread = (batch, run of R output rows, channel pair); lanes run along channel pairs (8-byte coalesced
 // loads, 4-byte stores).  R trades halo work ((2R+10)/R upsampled samples per output) against registers
@@ -107,43 +73,15 @@ __global__ __launch_bounds__(256) void act_op_kernel(const float* __restrict__ x
 #pragma unroll
       for (int i = 0; i < R + 12; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(j0 - 6 + i) * C);
       f32x2 o[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) o[r] = f32x2{0.f, 0.f};
-      // upsampled sample q (m = 2*j0 - 5 + q) feeds outputs r with 0 <= q - 2r <= 11 (down tap k = q - 2r,
-      // accumulated in ascending k as DownSample1d's conv does)
-#pragma unroll
-      for (int q = 0; q < 2 * R + 10; ++q) {
-        f32x2 u = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const int k = 2 * kk + (q & 1);
-          u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
-        }
-        const f32x2 sv = snake2(u * 2.0f, ear, h);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int k = q - 2 * r;
-          if (k >= 0 && k < 12) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv, o[r]);
-        }
-      }
+      act_run_interior<R>(win, f, ear, h, o);
 #pragma unroll
       for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
     } else {
       // sequence edges: replicate padding of the up (pad 5) and down (pad 5/6) filters
       for (int j = j0; j < j0 + R && j < T; ++j) {
-        f32x2 o = f32x2{0.f, 0.f};
-        for (int k = 0; k < 12; ++k) {
-          int m = 2 * j + k - 5;
-          m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
-          f32x2 u = f32x2{0.f, 0.f};
-          for (int kk = 0; kk < 6; ++kk) {
-            const int ku = 2 * kk + ((m & 1) ? 0 : 1);
-            int xi = (m + 5 - ku) / 2;
-            xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
-            u = fma2(f32x2{f.up[ku], f.up[ku]}, *reinterpret_cast<const f32x2*>(xb + (int64_t)xi * C), u);
-          }
-          o = fma2(f32x2{f.dn[k], f.dn[k]}, snake2(u * 2.0f, ear, h), o);
-        }
+        const f32x2 o = act_one_clamped(j, T, f, ear, h, [&](int i) {
+          return *reinterpret_cast<const f32x2*>(xb + (int64_t)i * C);
+        });
         op_store2<PREC>(yb + (int64_t)j * Cp, y_lo, o);
       }
     }
@@ -210,6 +148,8 @@ struct OpConvDev {
   int out_act, accumulate;
   float out_scale;
   int tiles_per_batch;
+  int tstride, tshift;  // tile i of a batch computes rows [i * tstride - tshift, + BM)
+  ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
 };
 
 constexpr int OC_AW = 48;       // window row stride (elements): conflict-free fragment reads from any start row
@@ -221,7 +161,7 @@ __device__ __forceinline__ int oc_boff(int r, int kq) { return r * 32 + ((kq ^ (
 // over the dead window/weight buffers, RG row groups (of TM*16 rows) at a time, and written as whole
 // BN-column row segments with 16-byte stores (residual read the same way).  VEC = N % 4 == 0.
 // PRE: prefetch the residual into registers at kernel start (narrow tiles whose tile fits one round).
-template <int BM, int BN, int WGM, int WGN, int PREC, int TPS, bool VEC>
+template <int BM, int BN, int WGM, int WGN, int PREC, int TPS, bool VEC, bool ACT>
 __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   constexpr int TM = BM / (WGM * 16);
   constexpr int TN = BN / (WGN * 16);
@@ -235,13 +175,15 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "4 waves");
   static_assert(TPS == 1 || TPS == 2, "1 or 2 taps per step");
   constexpr int AW_BYTES = 2 * NPA * WRM * OC_AW * 2, BS_BYTES = 2 * NPB * TPS * BN * 32 * 2;
-  constexpr int SMEM = AW_BYTES + BS_BYTES;
   constexpr int OTS = BN + 4;                                   // output tile row stride (floats)
+  constexpr int SMEM0 = AW_BYTES + BS_BYTES;
+  constexpr int SMEM = (ACT && BM * OTS * 4 > SMEM0) ? BM * OTS * 4 : SMEM0;  // ACT stages the whole tile                                   // output tile row stride (floats)
   constexpr int GROUP_BYTES = TM * 16 * OTS * 4;                // one row group of the tile
   constexpr int RG0 = SMEM / GROUP_BYTES;
   constexpr int RG = RG0 >= WGM ? WGM : (RG0 >= 1 ? RG0 : 1);   // row groups per epilogue round
   static_assert(GROUP_BYTES <= SMEM, "output row group must fit the LDS");
-  constexpr bool PRE = VEC && RG == WGM && (BM * BN / 4) <= 12 * 256;
+  static_assert(!ACT || (VEC && RG == WGM), "the fused activation needs the whole tile in LDS");
+  constexpr bool PRE = !ACT && VEC && RG == WGM && (BM * BN / 4) <= 12 * 256;
   constexpr int RPER = (BM * BN / 4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   auto Aw = reinterpret_cast<__bf16(*)[NPA][WRM * OC_AW]>(smem);
@@ -250,14 +192,14 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int b = blockIdx.x / P.tiles_per_batch;
-  const int t0 = (blockIdx.x - b * P.tiles_per_batch) * BM;
+  const int t0 = (blockIdx.x - b * P.tiles_per_batch) * P.tstride - P.tshift;
   const int col0 = blockIdx.y * BN;
   const int K = P.ksize;
   const int WR = BM + (K - 1) * P.dil;
   const int nC = P.Cp / 32;
   const int SPC = (K + TPS - 1) / TPS;  // steps per chunk
   const int nsteps = nC * SPC;
-  const int mrows = min(BM, P.T - t0);
+  const int mrows = min(BM, P.T - t0);  // (ACT tiles can start before t = 0; only the ACT epilogue sees them)
   const int64_t rowbase = (int64_t)b * P.T + t0;  // global output row of tile row 0
 
   // residual prefetch (narrow tiles): tile rows are one contiguous block of mrows * N floats
@@ -435,6 +377,50 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   }
 
   // epilogue
+  if constexpr (ACT) {
+    // v = conv + bias (+ res) for every tile row inside [0, T) -> LDS; fp32 out (if any) for the rows this
+    // tile owns; then Activation1d(v) of the owned rows -> operand planes (halo rows come from the tile)
+    float* ot = reinterpret_cast<float*>(smem);  // the K loop's last barrier retired every LDS read
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm * TM * 16 + i * 16 + (lane >> 4) * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = wn * TN * 16 + j * 16 + (lane & 15);
+          ot[m * OTS + n] = acc[i][j][r] + ((P.bias && n < P.N) ? P.bias[n] : 0.f);
+        }
+      }
+    __syncthreads();
+    const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
+    if (P.res || P.out) {
+      const int cq = P.N / 4;
+      for (int e = tid; e < BM * cq; e += 256) {
+        const int m = e / cq, n = (e - m * cq) * 4;
+        const int t = t0 + m;
+        if (t < 0 || t >= P.T) continue;
+        const int64_t go = ((int64_t)b * P.T + t) * P.N + n;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        if (P.res) {
+          const float4 rv = *reinterpret_cast<const float4*>(P.res + go);
+          v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+          *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+        }
+        if (P.out && t >= e_lo && t < e_hi) {
+          v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+          if (P.accumulate) {
+            const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+            v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+          }
+          *reinterpret_cast<float4*>(P.out + go) = v;
+        }
+      }
+      __syncthreads();
+    }
+    act_epilogue_tile<PREC>(ot, OTS, t0, e_lo, e_hi, P.T, P.act.Cp, 0, P.N, b, P.act, tid, 256);
+    return;
+  }
   if constexpr (VEC) {
     float* ot = reinterpret_cast<float*>(smem);  // the K loop's last barrier retired every LDS read
     for (int h0 = 0; h0 < WGM; h0 += RG) {
@@ -510,39 +496,60 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int TPS, bool VEC>
+template <int BM, int BN, int WGM, int WGN, int TPS, bool VEC, bool ACT>
 static void launch_opconv_v(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
   constexpr int TPS_SPLIT = BN >= 192 ? 1 : TPS;  // LDS: the split operands double both buffers
   if (prec == PREC_SPLIT)
-    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC>), grid, dim3(256), 0, s, Q);
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC, ACT>), grid, dim3(256), 0, s, Q);
   else if (prec == PREC_F16)
-    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, TPS, VEC>), grid, dim3(256), 0, s, Q);
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, TPS, VEC, ACT>), grid, dim3(256), 0, s, Q);
   else if (prec == PREC_F16W2)
-    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, TPS, VEC>), grid, dim3(256), 0, s, Q);
-  else hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_BF16, TPS, VEC>), grid, dim3(256), 0, s, Q);
+    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, TPS, VEC, ACT>), grid, dim3(256), 0, s, Q);
+  else hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_BF16, TPS, VEC, ACT>), grid, dim3(256), 0, s, Q);
 }
 
 template <int BM, int BN, int WGM, int WGN, int TPS>
-static void launch_opconv(const OpConvDev& P, int B, int prec, double flops, double bytes, hipStream_t s) {
+static int launch_opconv(const OpConvDev& P, int B, int prec, bool act, double flops, double bytes, hipStream_t s) {
   OpConvDev Q = P;
-  Q.tiles_per_batch = (P.T + BM - 1) / BM;
+  // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes BM conv rows and emits BM - 2*HALO
+  Q.tstride = act ? BM - 2 * ACT_EPI_HALO : BM;
+  Q.tshift = act ? ACT_EPI_HALO : 0;
+  Q.tiles_per_batch = (P.T + Q.tstride - 1) / Q.tstride;
   dim3 grid(B * Q.tiles_per_batch, (P.N + BN - 1) / BN);
   // LDS-staged epilogue for narrow layers (one tile spans N); wide layers store straight from the
   // accumulators (measured faster there: the LDS round trip costs more than the coalescing saves)
   const bool vec = P.N % 4 == 0 && P.N <= BN;
+  if (act && !vec) return set_error(ALCM_E_INVALID, "opconv: fused activation needs N % 4 == 0 and one column tile");
   void* tok = prof_start(s);
-  if (vec) launch_opconv_v<BM, BN, WGM, WGN, TPS, true>(Q, grid, prec, s);
-  else launch_opconv_v<BM, BN, WGM, WGN, TPS, false>(Q, grid, prec, s);
+  if (act) {
+    if constexpr (BN <= 96) launch_opconv_v<BM, BN, WGM, WGN, TPS, true, true>(Q, grid, prec, s);
+  } else if (vec) launch_opconv_v<BM, BN, WGM, WGN, TPS, true, false>(Q, grid, prec, s);
+  else launch_opconv_v<BM, BN, WGM, WGN, TPS, false, false>(Q, grid, prec, s);
   if (tok) {
-    char name[112];
-    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %d, %s>", BM, BN, WGM, WGN, prec, TPS,
-                  vec ? "true" : "false");
+    char name[128];
+    // the demangled rocprofv3 name of the instantiation (bench.py joins the two by name)
+    const int tps = (prec == PREC_SPLIT && BN >= 192) ? 1 : TPS;
+    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %d, %s, %s>", BM, BN, WGM, WGN, prec,
+                  tps, (vec || act) ? "true" : "false", act ? "true" : "false");
     prof_stop(tok, s, name, flops, bytes);
   }
+  return 0;
+}
+
+bool opconv_act_supported(int prec, int N, int Cp_in) {
+  if (std::getenv("ALCM_NO_ACT_FUSION")) return false;  // diagnostics / A-B
+  if (N % 4 || N <= 0) return false;
+  if (N <= 96) return true;  // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%
+  // wide layers (wconv, one 512-thread workgroup per CU): the activation's VALU work in the epilogue is
+  // serialised with the MFMA K loop and measured slower than the standalone act_op kernel,
+  // so it is opt-in (ALCM_WIDE_ACT_FUSION=1) for A/B runs
+  if (!std::getenv("ALCM_WIDE_ACT_FUSION")) return false;
+  return (prec == PREC_F16 || prec == PREC_BF16) && Cp_in % 64 == 0 && (N % 192 == 0 || N % 128 == 0);
 }
 
 int opconv(const alcm_opconv_args& a, hipStream_t s) {
-  if (!a.a || !a.w || !a.out || a.B <= 0 || a.T <= 0 || a.N <= 0 || a.ksize <= 0 || a.dil <= 0)
+  const bool act = a.act_plane != nullptr;
+  if (!a.a || !a.w || (!a.out && !act) || a.B <= 0 || a.T <= 0 || a.N <= 0 || a.ksize <= 0 || a.dil <= 0)
     return set_error(ALCM_E_INVALID, "opconv: bad arguments");
   if (a.Cp <= 0 || a.Cp % 32) return set_error(ALCM_E_INVALID, "opconv: Cp must be a positive multiple of 32");
   if ((a.ksize - 1) * a.dil > OC_HALO) return set_error(ALCM_E_INVALID, "opconv: receptive field too large");
@@ -552,8 +559,28 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   if ((((uintptr_t)a.a) & 15) || (((uintptr_t)a.w) & 15) || (a.a_lo_off % 8) || (a.w_lo_off % 8))
     return set_error(ALCM_E_INVALID, "opconv: operands must be 16-byte aligned");
   if (a.C <= 0 || a.C > a.Cp) return set_error(ALCM_E_INVALID, "opconv: C must be in (0, Cp]");
+  if (act) {
+    if (a.out_act || a.N % 2 || !a.act_alpha_exp || !a.act_inv_beta || !a.act_up_filter || !a.act_down_filter)
+      return set_error(ALCM_E_INVALID, "opconv: fused activation needs out_act == 0, even N and its parameters");
+    if (a.out && a.res && a.out == a.res) return set_error(ALCM_E_INVALID, "opconv: fused activation: out aliases res");
+    if ((((uintptr_t)a.act_plane) & 3) || (a.act_plane_lo_off % 2))
+      return set_error(ALCM_E_INVALID, "opconv: act_plane alignment");
+    if ((a.res && (((uintptr_t)a.res) & 15)) || (a.out && (((uintptr_t)a.out) & 15)) || a.N % 4)
+      return set_error(ALCM_E_INVALID, "opconv: fused activation needs 16-byte aligned res/out and N % 4 == 0");
+  }
   OpConvDev P{};
   P.a = (const u16*)a.a; P.a_lo = a.a_lo_off;
+  if (act) {
+    P.act.plane = (u16*)a.act_plane;
+    P.act.plane_lo = a.act_plane_lo_off;
+    P.act.Cp = round_up(a.N, 32);
+    P.act.aexp = a.act_alpha_exp;
+    P.act.ibeta = a.act_inv_beta;
+    for (int k = 0; k < 12; ++k) {
+      P.act.f.up[k] = a.act_up_filter[k];
+      P.act.f.dn[k] = a.act_down_filter[k];
+    }
+  }
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   // planes of the packed weight: bf16 hi | bf16 lo | fp16 hi | fp16 lo, w_lo_off apart
   const bool f16 = a.prec == PREC_F16 || a.prec == PREC_F16W2;
@@ -565,20 +592,24 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const int npa = a.prec == PREC_SPLIT ? 2 : 1, npb = (a.prec == PREC_SPLIT || a.prec == PREC_F16W2) ? 2 : 1;
   const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;
   const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
-                       M * a.N * 4.0 * (1 + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0));
-  if (wconv_try(a, P.w, flops, bytes, s)) {
+                       M * a.N * 4.0 * ((a.out ? 1 : 0) + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0)) +
+                       (act ? M * round_up(a.N, 32) * 2.0 * npa : 0.0);
+  if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s)) {
     ALCM_HIP(hipGetLastError());
     return 0;
   }
   const int N = a.N;
   // one tap per K step (two taps per step measured slower: the larger weight buffers cost occupancy)
-  //                                               BM   BN  WGM WGN TPS
-  if (N % 192 == 0 && N % 128 != 0) launch_opconv<128, 192, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
-  else if (N % 128 == 0) launch_opconv<128, 128, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 48) launch_opconv<128, 96, 2, 2, 1>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 32) launch_opconv<256, 48, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
-  else if (N > 16) launch_opconv<256, 32, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
-  else launch_opconv<256, 16, 4, 1, 1>(P, a.B, a.prec, flops, bytes, s);
+  //                                                      BM   BN  WGM WGN TPS
+  int rc;
+  if (act && N > 96) rc = set_error(ALCM_E_INVALID, "opconv: fused activation on N > 96 needs the wide kernel");
+  else if (N % 192 == 0 && N % 128 != 0) rc = launch_opconv<128, 192, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else if (N % 128 == 0) rc = launch_opconv<128, 128, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else if (N > 48) rc = launch_opconv<128, 96, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else if (N > 32) rc = launch_opconv<256, 48, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else if (N > 16) rc = launch_opconv<256, 32, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else rc = launch_opconv<256, 16, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  if (rc) return rc;
   ALCM_HIP(hipGetLastError());
   return 0;
 }

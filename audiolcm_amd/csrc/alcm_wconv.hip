@@ -22,6 +22,7 @@
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
+#include "alcm_actepi.h"
 
 namespace alcm {
 
@@ -41,6 +42,8 @@ struct WConvDev {
   float out_scale;
   int accumulate;
   int tiles_per_batch, tiles_n, nwg;
+  int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
+  ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
 };
 
 constexpr int WC_BM = 256;
@@ -51,7 +54,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
 }
 
-template <int BN, int PREC, int VAR>
+template <int BN, int PREC, int VAR, bool ACT>
 __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
   constexpr int TN = BN / 64;            // 16-col fragments per wave (wave covers BN/4 columns)
   constexpr int BPW = BN / 64;           // weight DMA instructions per wave per step (BN/8 rows-of-8 / 8 waves)
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
   const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
   const int mt = wid / P.tiles_n, nt = wid - mt * P.tiles_n;
   const int b = mt / P.tiles_per_batch;
-  const int t0 = (mt - b * P.tiles_per_batch) * WC_BM;
+  const int t0 = (mt - b * P.tiles_per_batch) * P.tstride - P.tshift;
   const int col0 = nt * BN;
   const int K = P.ksize, Cp = P.Cp;
   const int WR = WC_BM + (K - 1) * P.dil;
@@ -189,6 +192,56 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if constexpr (ACT) {
+    // v = conv + bias (+ res) -> LDS, one half of the tile's columns at a time (all 256 rows: the
+    // activation needs the halo rows); fp32 out (if any) for the owned rows; Activation1d -> planes
+    constexpr int HC = BN / 2;      // columns per half
+    constexpr int OTS = HC + 4;
+    float* ot = reinterpret_cast<float*>(smem);
+    const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
+    for (int h = 0; h < 2; ++h) {
+      if ((wn >> 1) == h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int nl = (wn & 1) * (BN / 4) + j * 16 + (lane & 15);
+              ot[(wm * 128 + i * 16 + (lane >> 4) * 4 + r) * OTS + nl] =
+                  acc[i][j][r] + (P.bias ? P.bias[col0 + h * HC + nl] : 0.f);
+            }
+      }
+      __syncthreads();
+      if (P.res || P.out) {
+        constexpr int cq = HC / 4;
+        for (int e = tid; e < WC_BM * cq; e += 512) {
+          const int m = e / cq, n = (e - m * cq) * 4;
+          const int t = t0 + m;
+          if (t < 0 || t >= P.T) continue;
+          const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + h * HC + n;
+          float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+          if (P.res) {
+            const float4 rv = *reinterpret_cast<const float4*>(P.res + go);
+            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+            *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+          }
+          if (P.out && t >= e_lo && t < e_hi) {
+            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+            if (P.accumulate) {
+              const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+            }
+            *reinterpret_cast<float4*>(P.out + go) = v;
+          }
+        }
+        __syncthreads();
+      }
+      act_epilogue_tile<PREC>(ot, OTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 512);
+      __syncthreads();
+    }
+    return;
+  }
   if constexpr ((VAR & 4) != 0) {
     // LDS-staged epilogue: one 128-row half of the tile at a time goes through LDS (the K loop's last
     // barrier retired every fragment read) and leaves as whole row segments with 16-B residual loads
@@ -264,23 +317,29 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
 
 // Eligible: single-plane precisions, N a multiple of 128, Cp a multiple of 64, 2 <= k, (k-1)d <= 64,
 // no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
-int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
-  const char* env = std::getenv("ALCM_WCONV");  // diagnostics / A-B: ALCM_WCONV=0 uses opconv_kernel
-  int var = env ? std::atoi(env) : 5;  // default: plain K loop + LDS-staged epilogue (measured best)
-  if (var <= 0) return 0;
+int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
+              hipStream_t s) {
+  const char* env = std::getenv("ALCM_WCONV");  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop
+  const int var = env ? std::atoi(env) : 5;      // default: plain K loop + LDS-staged epilogue (measured best)
+  const bool act = actepi != nullptr;
+  if (var <= 0 && !act) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.Cp % 64 || a.ksize < 2 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
   const int BN = a.N % 192 == 0 ? 192 : (a.N % 128 == 0 ? 128 : 0);
   if (!BN) return 0;
-  if ((int64_t)a.B * a.T < 4 * WC_BM) return 0;
+  if (!act && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
-  if ((var & 4) && !(al16(a.bias) && al16(a.res) && al16(a.out))) var &= 3;  // small problems: the 128-row kernel fills the chip better
+  if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   WConvDev P{};
   P.a = (const u16*)a.a;
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
-  P.tiles_per_batch = (a.T + WC_BM - 1) / WC_BM;
+  // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 256 conv rows and emits 256 - 2 * HALO
+  P.tstride = act ? WC_BM - 2 * ACT_EPI_HALO : WC_BM;
+  P.tshift = act ? ACT_EPI_HALO : 0;
+  if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
+  P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
   P.tiles_n = a.N / BN;
   const int64_t nwg = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
   if (nwg >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
@@ -288,26 +347,24 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   void* tok = prof_start(s);
   const dim3 grid((unsigned)nwg), blk(512);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, blk, 0, s, P); };
-  auto pick = [&](auto vc) {
+  auto pick = [&](auto vc, auto ac) {
     constexpr int V = decltype(vc)::value;
+    constexpr bool A = decltype(ac)::value;
     if (BN == 192) {
-      if (a.prec == PREC_F16) go(wconv_kernel<192, PREC_F16, V>);
-      else go(wconv_kernel<192, PREC_BF16, V>);
+      if (a.prec == PREC_F16) go(wconv_kernel<192, PREC_F16, V, A>);
+      else go(wconv_kernel<192, PREC_BF16, V, A>);
     } else {
-      if (a.prec == PREC_F16) go(wconv_kernel<128, PREC_F16, V>);
-      else go(wconv_kernel<128, PREC_BF16, V>);
+      if (a.prec == PREC_F16) go(wconv_kernel<128, PREC_F16, V, A>);
+      else go(wconv_kernel<128, PREC_BF16, V, A>);
     }
   };
-  switch (var) {
-    case 2: pick(std::integral_constant<int, 1>{}); break;
-    case 3: pick(std::integral_constant<int, 2>{}); break;
-    case 5: pick(std::integral_constant<int, 4>{}); break;
-    case 7: pick(std::integral_constant<int, 6>{}); break;
-    default: pick(std::integral_constant<int, 0>{}); break;
-  }
+  const int V = (!act && var == 7) ? 6 : 4;
+  if (act) pick(std::integral_constant<int, 4>{}, std::true_type{});
+  else if (V == 6) pick(std::integral_constant<int, 6>{}, std::false_type{});
+  else pick(std::integral_constant<int, 4>{}, std::false_type{});
   if (tok) {
-    char name[80];
-    std::snprintf(name, sizeof(name), "alcm::wconv_kernel<%d, %d>", BN, a.prec);
+    char name[80];  // the demangled rocprofv3 name of the instantiation
+    std::snprintf(name, sizeof(name), "alcm::wconv_kernel<%d, %d, %d, %s>", BN, a.prec, V, act ? "true" : "false");
     prof_stop(tok, s, name, flops, bytes);
   }
   return 1;

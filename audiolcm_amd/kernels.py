@@ -377,8 +377,12 @@ def activation1d_op(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
 
 def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
-           accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None) -> torch.Tensor:
-    """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...)."""
+           accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
+           act: Optional[tuple] = None, fp32_out: bool = True):
+    """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
+
+    act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
+    planes (NP, B, T, round_up(N, 32)) from the fused epilogue -> (out or None, planes)."""
     npl, B, T, Cp = planes.shape
     assert planes.dtype == torch.int16 and planes.is_contiguous()
     N, cin, k = w.shape
@@ -392,8 +396,29 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     a.w, a.w_lo_off, a.kpad, a.N = ptr(packed.data), packed.lo_off, packed.kpad, N
     a.bias = ptr(bias)
     a.res = ptr(residual.contiguous()) if residual is not None else None
-    out = accumulate_into if accumulate_into is not None else torch.empty((B, T, N), device=planes.device)
+    if accumulate_into is not None:
+        out = accumulate_into
+    else:
+        out = torch.empty((B, T, N), device=planes.device) if (fp32_out or act is None) else None
     a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
         out_scale, int(prec)
+    keep = []
+    if act is not None:
+        alpha, beta, fu, fd = act
+        ae, ib = snake_params(alpha, beta)
+        ae, ib = ae.contiguous(), ib.contiguous()
+        fu = fu.detach().reshape(-1).float().cpu().contiguous()
+        fd = fd.detach().reshape(-1).float().cpu().contiguous()
+        cpo = _round_up(N, 32)
+        nplo = 2 if prec == _hip.PREC_SPLIT else 1
+        y = torch.empty((nplo, B, T, cpo), dtype=torch.int16, device=planes.device)
+        keep = [ae, ib, fu, fd]
+        a.act_plane, a.act_plane_lo_off = ptr(y), B * T * cpo
+        a.act_alpha_exp, a.act_inv_beta = ptr(ae), ptr(ib)
+        a.act_up_filter = fu.data_ptr()
+        a.act_down_filter = fd.data_ptr()
     check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
+    del keep
+    if act is not None:
+        return out, y
     return out

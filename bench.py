@@ -144,12 +144,16 @@ def main():
         else:
             ach, peak, unit = dom["bytes"] / sec / 1e9, _hip.PEAK_HBM_BYTES / 1e9, "GB/s"
         roofline = dict(bound="mfma" if mfma else "hbm", achieved=round(ach, 2), peak=peak, unit=unit,
-                        frac=round(ach / peak, 4), traffic=pmc_traffic(dom["name"]), kernel=dom["name"], launches=dom["launches"],
+                        frac=round(ach / peak, 4), traffic=None, kernel=dom["name"], launches=dom["launches"],
                         avg_launch_us=round(1e3 * dom["total_ms"] / dom["launches"], 2),
                         per_launch_algorithmic=round((dom["flops"] if mfma else dom["bytes"]) / dom["launches"], 1),
                         kernel_share_of_gpu_time=round(dom["total_ms"] / max(gpu_ms, 1e-9), 4),
                         path_roofline_frac=round(sum(p["roof_ms"] for p in prof) / (1e3 * dt), 4),
                         path_roofline_note="sum over all kernel launches of max(F/2.5PF, B/8TB/s) / measured wall")
+        tr = pmc_traffic(dom["name"])
+        if tr:  # HBM bytes per launch from the committed PMC passes of this kernel
+            roofline["traffic"] = tr["bytes_per_launch"]
+            roofline["traffic_source"] = tr["source"]
     line = dict(metric=METRIC, value=round(value, 2), unit="audio-s/s", n_gpus=world, steps=a.steps,
                 warmup=a.warmup, ms_per_step=round(1e3 * dt / a.steps, 2), higher_is_better=True, scaling="weak",
                 vs_baseline=None,
@@ -174,6 +178,10 @@ def main():
     if rank == 0:
         line["kernels"] = sorted(({k: (round(v, 3) if isinstance(v, float) else v) for k, v in p.items()}
                                   for p in prof), key=lambda p: -p["total_ms"])[:8]
+        if os.environ.get("ALCM_BENCH_ALL_KERNELS"):
+            for p in sorted(prof, key=lambda p: -p["total_ms"]):
+                print(f"{p['name'][:72]:72s} n={p['launches']:5d} {p['total_ms'] / a.steps:8.3f} ms/step "
+                      f"roof {p['roof_ms'] / a.steps:7.3f}", file=sys.stderr)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -187,6 +187,18 @@ typedef struct alcm_opconv_args {
   int out_act, accumulate;
   float out_scale;
   int prec;
+  /* optional fused Activation1d epilogue (alias_free_torch/act.py:23-27 applied to v = conv + bias (+ res)):
+   * when act_plane != NULL the kernel also writes Activation1d(v) as MFMA operand planes [B][T][Cp'] with
+   * Cp' = round_up(N, 32), in the format `prec` reads (SPLIT: lo plane act_plane_lo_off elements after hi),
+   * ready for the next conv.  `out` may then be NULL (no fp32 output).  Tiles recompute 8 halo rows, so
+   * `out` must not overlap `res`.  alpha_exp / inv_beta are device arrays of N (exp(alpha),
+   * 1/(exp(beta)+1e-9)); the 12-tap filters are HOST arrays.  Requires out_act == 0 and N even. */
+  void* act_plane;
+  int64_t act_plane_lo_off;
+  const float* act_alpha_exp;
+  const float* act_inv_beta;
+  const float* act_up_filter;
+  const float* act_down_filter;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 

@@ -303,6 +303,43 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
     assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("C,T,k,dil,prec", [(24, 1000, 11, 5, 3), (48, 700, 7, 3, 3), (96, 500, 3, 1, 3),
+                                            (96, 333, 11, 5, 1), (24, 250, 3, 1, 2), (48, 37, 7, 1, 0),
+                                            (768, 600, 11, 5, 2), (384, 1100, 7, 3, 2), (192, 1500, 3, 1, 0),
+                                            (192, 90, 7, 3, 2)])
+@pytest.mark.parametrize("res", [False, True])
+def test_opconv_fused_activation(K, C, T, k, dil, prec, res):
+    """Fused Activation1d epilogue (overlapping tiles, 8 halo rows) == fp32 conv output followed by the
+    standalone act_op kernel: the same fp32 values go through the same activation code, so the planes match
+    bit for bit, and the fp32 output (owned rows only) matches the unfused conv."""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B = 2
+    x = _r((B, T, C), 90)
+    w, bias = _r((C, C, k), 91, 0.7 / np.sqrt(C * k)), _r((C,), 92, 0.05)
+    r = dev(_r((B, T, C), 93)) if res else None
+    a, bt = dev(_r((C,), 94, 0.3)), dev(_r((C,), 95, 0.3))
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    pl = K.operand_planes(dev(x), prec)
+    y_ref = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r)
+    pl_ref = K.activation1d_op(y_ref, a, bt, f, f, prec)
+    y, pl2 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r, act=(a, bt, f, f))
+    assert pl2.shape == pl_ref.shape
+
+    def dec(p):  # operand planes -> fp32 values
+        p = p.cpu()
+        if prec in (2, 3):
+            return p[0].view(torch.float16).float()
+        v = p[0].view(torch.bfloat16).float()
+        return v + p[1].view(torch.bfloat16).float() if prec == 1 else v
+
+    # (the unfused call may take a kernel with another K order for small B*T: fp32 rounding only)
+    assert rel_l2(y.cpu().numpy(), y_ref.cpu().numpy()) < 1e-6
+    assert rel_l2(dec(pl2).numpy(), dec(pl_ref).numpy()) < 1e-5
+    assert torch.all(pl2.cpu()[..., C:] == 0)
+    _, pl3 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r, act=(a, bt, f, f), fp32_out=False)
+    assert torch.equal(pl3.cpu(), pl2.cpu())
+
+
 @pytest.mark.parametrize("prec", [1, 2, 3])
 def test_opconv_post_tanh_accumulate(K, prec):
     """conv_post shape (N = 1, k7) with tanh, and the accumulate/out_scale epilogue (resblock mean)."""
