@@ -88,6 +88,7 @@ _SIGS = [
     ("alcm_amp_conv", C.c_int, [C.POINTER(AmpArgs), vp]),
     ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
+    ("alcm_flash_attention", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
     ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_lcm_step_cfg", C.c_int, [fp, fp, fp, C.c_float, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_sincos_embedding", C.c_int, [fp, C.c_float, fp, C.c_int, C.c_int, C.c_int, fp, vp]),

@@ -1,0 +1,198 @@
+// Fused multi-head self-attention for the DiT (CrossAttention used as self-attention,
+// ldm/modules/new_attention.py:89-130): O = softmax(Q K^T * dh^-1/2) V per (batch, head), with the
+// scores kept on chip (flash-attention style online softmax) instead of an (L x L) round trip through HBM.
+//
+// gfx950 layout (16x16x32 MFMAs, 64-lane waves, fp32 accumulation):
+//   * a workgroup = 4 waves = 64 queries of one (b, head); each wave owns 16 queries;
+//   * scores are computed transposed, S^T = K Q^T (A = K tile from LDS, B = the wave's Q fragments held in
+//     registers), so a lane's accumulators all belong to ONE query (column lane & 15): the running max /
+//     sum of the online softmax need only a 4-lane reduction (lanes l, l^16, l^32, l^48);
+//   * O^T = V^T P^T reuses the S^T accumulators directly as the B operand: the 8 keys a lane holds for a
+//     32-key slice are {4g..4g+3, 16+4g..16+4g+3} (g = lane >> 4) instead of 8g..8g+7, and the A operand
+//     (V^T from LDS) is read with the same key permutation, so P never moves between lanes;
+//   * K and V^T tiles (64 keys) are converted from the fp32 qkv rows to the MFMA operand format while they
+//     are staged into LDS (padded row strides: conflict-free fragment reads).
+// Operands are rounded to fp16 (PREC_F16) or bf16 (PREC_BF16) exactly as the GEMM path rounds them; the
+// probabilities are rounded after the exp (unnormalised, in (0, 1]) and the 1/l normalisation is applied
+// to the fp32 output.
+#include <cmath>
+#include <cstdio>
+
+#include "alcm_common.h"
+#include "alcm_internal.h"
+
+namespace alcm {
+
+constexpr int FA_Q = 64;       // queries per workgroup
+constexpr int FA_KT = 64;      // keys per tile
+constexpr int FA_DK = 96;      // head dim padded for the QK^T contraction (3 x 32)
+constexpr int FA_DV = 80;      // head dim padded for the PV output rows (5 x 16)
+constexpr int FA_KS = 104;     // K tile row stride (elements): 208 B
+constexpr int FA_VS = 68;      // V^T tile row stride (elements): 136 B
+
+template <int PREC>
+__device__ __forceinline__ u16 fa_cvt(float v) {
+  if constexpr (PREC == PREC_F16) return __builtin_bit_cast(u16, (_Float16)v);
+  else return __builtin_bit_cast(u16, (__bf16)v);
+}
+
+template <int PREC>
+__global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict__ qkv, float* __restrict__ O, int L,
+                                                         int H, int nh, int dh, float scale) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[FA_KT * FA_KS];
+  __shared__ __attribute__((aligned(16))) u16 Vt[FA_DV * FA_VS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, cq = lane & 15;
+  const int z = blockIdx.y, b = z / nh, h = z - b * nh;
+  const int q0 = blockIdx.x * FA_Q + wave * 16;
+  const int64_t rs = 3 * (int64_t)H;  // qkv row stride
+  const float* base = qkv + (int64_t)b * L * rs + h * dh;
+
+  // Q fragments (B operand of S^T): lane holds Q[q0 + cq][32 ks + 8 g .. + 7]
+  bf16x8 qf[3];
+  {
+    const int q = q0 + cq;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      u16 e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 32 * ks + 8 * g + j;
+        e[j] = fa_cvt<PREC>((q < L && d < dh) ? base[(int64_t)q * rs + d] : 0.f);
+      }
+      qf[ks] = __builtin_bit_cast(bf16x8, e);
+    }
+  }
+  f32x4 o[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int nkt = (L + FA_KT - 1) / FA_KT;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * FA_KT;
+    __syncthreads();  // previous tile's fragment reads retired
+    // stage K [key][dim] and V^T [dim][key] (zero padding beyond L / dh)
+    for (int e = tid; e < FA_KT * (FA_DK / 4); e += 256) {
+      const int kr = e / (FA_DK / 4), d4 = (e - kr * (FA_DK / 4)) * 4;
+      const int key = k0 + kr;
+      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (key < L && d4 < dh) {
+        const float* r = base + (int64_t)key * rs + d4;
+        kv = *reinterpret_cast<const float4*>(r + H);
+        vv = *reinterpret_cast<const float4*>(r + 2 * H);
+      }
+      uint2 kp;
+      kp.x = (uint32_t)fa_cvt<PREC>(kv.x) | ((uint32_t)fa_cvt<PREC>(kv.y) << 16);
+      kp.y = (uint32_t)fa_cvt<PREC>(kv.z) | ((uint32_t)fa_cvt<PREC>(kv.w) << 16);
+      *reinterpret_cast<uint2*>(&Ks[kr * FA_KS + d4]) = kp;
+      if (d4 < FA_DV) {
+        Vt[(d4 + 0) * FA_VS + kr] = fa_cvt<PREC>(vv.x);
+        Vt[(d4 + 1) * FA_VS + kr] = fa_cvt<PREC>(vv.y);
+        Vt[(d4 + 2) * FA_VS + kr] = fa_cvt<PREC>(vv.z);
+        Vt[(d4 + 3) * FA_VS + kr] = fa_cvt<PREC>(vv.w);
+      }
+    }
+    __syncthreads();
+    // S^T block kb: rows = keys 16 kb + (4g + r), column = query cq
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * kb + cq) * FA_KS + 32 * ks + 8 * g]);
+        s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
+      }
+    }
+    // online softmax over this tile's keys (per query = per lane column)
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * kb + 4 * g + r;
+        const float v = key < L ? s[kb][r] * scale : -INFINITY;
+        s[kb][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = __expf(m - mn);  // 0 on the first tile (m = -inf)
+    m = mn;
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(s[kb][r] - mn);
+        s[kb][r] = p;
+        psum += p;
+      }
+    l = l * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) o[i] *= alpha;
+    // O^T += V^T P^T over two 32-key slices
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u16 pe[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pe[r] = fa_cvt<PREC>(s[2 * ks][r]);
+        pe[4 + r] = fa_cvt<PREC>(s[2 * ks + 1][r]);
+      }
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, pe);
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const u16* vr = &Vt[(16 * db + cq) * FA_VS + 32 * ks + 4 * g];
+        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+        const uint4 vv = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        o[db] = mfma16<PREC>(__builtin_bit_cast(bf16x8, vv), pf, o[db]);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  const int q = q0 + cq;
+  if (q >= L) return;
+  const float inv = 1.0f / l;
+  float* orow = O + ((int64_t)b * L + q) * H + h * dh;
+#pragma unroll
+  for (int db = 0; db < 5; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = 16 * db + 4 * g + r;
+      if (d < dh) orow[d] = o[db][r] * inv;
+    }
+}
+
+// qkv: (B, L, 3H) fp32 rows [q | k | v], head h at columns h*dh; O: (B, L, H) fp32
+int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s) {
+  if (!qkv || !O || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
+  const int dh = H / nh;
+  if (dh > 72 || dh % 4 || H % 4) return set_error(ALCM_E_INVALID, "flash_attention: head dim must be <= 72, % 4");
+  if (prec != PREC_F16 && prec != PREC_BF16) return set_error(ALCM_E_INVALID, "flash_attention: F16 or BF16 only");
+  if (((uintptr_t)qkv) & 15) return set_error(ALCM_E_INVALID, "flash_attention: qkv must be 16-byte aligned");
+  const dim3 grid((L + FA_Q - 1) / FA_Q, B * nh);
+  const float scale = 1.0f / std::sqrt((float)dh);
+  void* tok = prof_start(s);
+  if (prec == PREC_F16) hipLaunchKernelGGL(flash_attn_kernel<PREC_F16>, grid, dim3(256), 0, s, qkv, O, L, H, nh, dh, scale);
+  else hipLaunchKernelGGL(flash_attn_kernel<PREC_BF16>, grid, dim3(256), 0, s, qkv, O, L, H, nh, dh, scale);
+  if (tok) {
+    char name[64];
+    std::snprintf(name, sizeof(name), "alcm::flash_attn_kernel<%d>", prec);
+    const double z = (double)B * nh;
+    prof_stop(tok, s, name, z * 4.0 * L * (double)L * dh, (double)B * L * (3.0 * H + H) * 4.0);
+  }
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace alcm
+
+extern "C" int alcm_flash_attention(const float* qkv, float* out, int B, int L, int H, int heads, int prec,
+                                    alcm_stream_t stream) {
+  return alcm::flash_attention(qkv, out, B, L, H, heads, prec, (hipStream_t)stream);
+}

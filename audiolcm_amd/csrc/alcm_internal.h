@@ -43,7 +43,10 @@ int amp_conv(const alcm_amp_args& a, hipStream_t s);
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
+int nconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
+              hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
+int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s);
 // whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
 bool opconv_act_supported(int prec, int N, int Cp_in);
 // actepi: const ActEpiDev* (alcm_actepi.h) or nullptr

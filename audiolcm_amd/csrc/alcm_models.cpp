@@ -7,6 +7,7 @@
 // is only used at the boundary (latents x/z/eps, mel, waveform) and is read/written through
 // strided GEMM operands, so no transpose kernels run.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -563,6 +564,9 @@ static DitWs plan_dit(const DitW& D, Bump& bp, int B, int T) {
 // attention core over a fused qkv buffer (B, L, 3H): O[b, t, h*dh + d] (new_attention.py:107-126)
 static int dit_attention(hipStream_t s, int split, const DitW& D, int B, int L, const float* qkv, float* S, float* O) {
   const int H = D.hidden, nh = D.heads, dh = H / nh, Lp = round_up(L, 8);
+  // single-rounding policies: fused kernel, scores never leave the chip (alcm_attn.hip)
+  if ((split == PREC_F16 || split == PREC_BF16) && dh <= 72 && dh % 4 == 0 && !std::getenv("ALCM_NO_FLASH"))
+    return flash_attention(qkv, O, B, L, H, nh, split, s);
   alcm_gemm_args g;
   std::memset(&g, 0, sizeof(g));
   // S = (Q K^T) * dh^-1/2, batched over z = b*nh + head

@@ -499,9 +499,11 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
 template <int BM, int BN, int WGM, int WGN, int TPS, bool VEC, bool ACT>
 static void launch_opconv_v(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
   constexpr int TPS_SPLIT = BN >= 192 ? 1 : TPS;  // LDS: the split operands double both buffers
-  if (prec == PREC_SPLIT)
-    hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC, ACT>), grid, dim3(256), 0, s, Q);
-  else if (prec == PREC_F16)
+  constexpr bool SPLIT_FITS = 2 * 2 * (BM + OC_HALO) * OC_AW * 2 + 2 * 2 * TPS_SPLIT * BN * 32 * 2 <= 160 * 1024;
+  if (prec == PREC_SPLIT) {
+    if constexpr (SPLIT_FITS)
+      hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC, ACT>), grid, dim3(256), 0, s, Q);
+  } else if (prec == PREC_F16)
     hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, TPS, VEC, ACT>), grid, dim3(256), 0, s, Q);
   else if (prec == PREC_F16W2)
     hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16W2, TPS, VEC, ACT>), grid, dim3(256), 0, s, Q);
@@ -534,6 +536,13 @@ static int launch_opconv(const OpConvDev& P, int B, int prec, bool act, double f
     prof_stop(tok, s, name, flops, bytes);
   }
   return 0;
+}
+
+// narrow-layer tile variant (diagnostics / A-B): ALCM_OPCONV_TILE=0 default, 1 = twice the rows per tile,
+// 2 = twice the rows and two taps per K step
+static int tile_variant(int prec) {
+  const char* e = std::getenv("ALCM_OPCONV_TILE");
+  return (e && prec != PREC_SPLIT) ? std::atoi(e) : 0;  // the split operands need the default tiles' LDS
 }
 
 bool opconv_act_supported(int prec, int N, int Cp_in) {
@@ -594,7 +603,8 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
                        M * a.N * 4.0 * ((a.out ? 1 : 0) + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0)) +
                        (act ? M * round_up(a.N, 32) * 2.0 * npa : 0.0);
-  if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s)) {
+  if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s) ||
+      nconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s)) {
     ALCM_HIP(hipGetLastError());
     return 0;
   }
@@ -605,9 +615,22 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   if (act && N > 96) rc = set_error(ALCM_E_INVALID, "opconv: fused activation on N > 96 needs the wide kernel");
   else if (N % 192 == 0 && N % 128 != 0) rc = launch_opconv<128, 192, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
   else if (N % 128 == 0) rc = launch_opconv<128, 128, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
-  else if (N > 48) rc = launch_opconv<128, 96, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
-  else if (N > 32) rc = launch_opconv<256, 48, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
-  else if (N > 16) rc = launch_opconv<256, 32, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  else if (N > 48) {
+    const int v = tile_variant(a.prec);
+    if (v == 1) rc = launch_opconv<256, 96, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+    else if (v == 2) rc = launch_opconv<256, 96, 4, 1, 2>(P, a.B, a.prec, act, flops, bytes, s);
+    else rc = launch_opconv<128, 96, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  } else if (N > 32) {
+    const int v = tile_variant(a.prec);
+    if (v == 1) rc = launch_opconv<512, 48, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+    else if (v == 2) rc = launch_opconv<512, 48, 4, 1, 2>(P, a.B, a.prec, act, flops, bytes, s);
+    else rc = launch_opconv<256, 48, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  } else if (N > 16) {
+    const int v = tile_variant(a.prec);
+    if (v == 1) rc = launch_opconv<512, 32, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+    else if (v == 2) rc = launch_opconv<512, 32, 4, 1, 2>(P, a.B, a.prec, act, flops, bytes, s);
+    else rc = launch_opconv<256, 32, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
+  }
   else rc = launch_opconv<256, 16, 4, 1, 1>(P, a.B, a.prec, act, flops, bytes, s);
   if (rc) return rc;
   ALCM_HIP(hipGetLastError());

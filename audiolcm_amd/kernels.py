@@ -422,3 +422,14 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     if act is not None:
         return out, y
     return out
+
+
+def flash_attention(qkv: torch.Tensor, heads: int, prec: int) -> torch.Tensor:
+    """(B, L, 3H) fp32 [q | k | v] rows -> (B, L, H) multi-head softmax(q k^T / sqrt(dh)) v (fused kernel)."""
+    B, L, H3 = qkv.shape
+    H = H3 // 3
+    qkv = qkv.contiguous()
+    out = torch.empty((B, L, H), device=qkv.device)
+    check(lib().alcm_flash_attention(ptr(qkv), ptr(out), B, L, H, heads, int(prec), stream_handle()),
+          "flash_attention")
+    return out

@@ -202,6 +202,13 @@ typedef struct alcm_opconv_args {
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 
+/* alcm_flash_attention: multi-head self-attention of the DiT (CrossAttention with context = x,
+ * ldm/modules/new_attention.py:89-130, the q/k/v projections already applied):
+ * out[b, i, h*dh:(h+1)*dh] = softmax_j(q_i . k_j * dh^-1/2) v_j per head, scores kept on chip.
+ * qkv: (B, L, 3H) fp32 DEVICE rows [q | k | v] (16-byte aligned), out: (B, L, H) fp32; dh = H / heads <= 72;
+ * prec: ALCM PREC_F16 (2) or PREC_BF16 (0) operand rounding of q, k, v and the probabilities. */
+int alcm_flash_attention(const float* qkv, float* out, int B, int L, int H, int heads, int prec, alcm_stream_t stream);
+
 /* ---------------------------------------------------------------- LCM scheduler pieces */
 /* coeffs (HOST array of 6): {sqrt_a, sqrt_b, c_out, c_skip, sqrt_a_prev, sqrt_b_prev};
  * noise may be NULL (final step: prev_out = denoised) */

@@ -169,6 +169,31 @@ def bench_wconv(B=32):
                 print(f"C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line) + f" | max|diff| {diff:.2e}", flush=True)
 
 
+def bench_tail(B=32):
+    """BigVGAN tail (C = 96/48/24) conv launches as the model runs them: conv1 (dilated) + fused Activation1d
+    epilogue, conv2 + residual (+ fused Activation1d): opconv_kernel (ALCM_NCONV=0) vs nconv_kernel"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T, p in ((96, 39936, 3), (48, 79872, 3), (24, 159744, 3)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        pl = K.operand_planes(x, p)
+        cp = (C + 31) // 32 * 32
+        for k, d in ((11, 5), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
+            line = []
+            for v in os.environ.get("NCONV_VARS", "0,1").split(","):
+                os.environ["ALCM_NCONV"] = v
+                ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
+                ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
+                ms3 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
+                line.append(f"v{v}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
+            os.environ.pop("ALCM_NCONV")
+            print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
+
+
 def bench_op1(B=32):
     """one act_op + one opconv launch per tail/wide shape (target of rocprofv3 --pmc passes)"""
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
@@ -189,4 +214,4 @@ if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["amp", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
+        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()

@@ -138,6 +138,20 @@ def test_attention_products(K, Z, L, d):
     assert rel_l2(o.numpy(), torch.einsum("bij,bjd->bid", p, v).numpy()) < SPLIT_TOL
 
 
+@pytest.mark.parametrize("B,L,heads,dh", [(2, 467, 8, 72), (1, 40, 8, 72), (3, 130, 4, 64), (1, 1, 2, 36)])
+@pytest.mark.parametrize("prec", [2, 0])
+def test_flash_attention(K, B, L, heads, dh, prec):
+    """Fused attention (online softmax, scores on chip) vs fp32 softmax(q k^T / sqrt(dh)) v."""
+    H = heads * dh
+    qkv = _r((B, L, 3 * H), 100, 1.5)
+    q, k, v = qkv.split(H, dim=-1)
+    sh = lambda t: t.reshape(B, L, heads, dh).permute(0, 2, 1, 3)
+    att = torch.softmax(sh(q) @ sh(k).transpose(-1, -2) / dh ** 0.5, dim=-1) @ sh(v)
+    ref = att.permute(0, 2, 1, 3).reshape(B, L, H)
+    y = K.flash_attention(dev(qkv), heads, prec).cpu()
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+
+
 def test_linear_and_layer_norm(K):
     x = _r((3, 77, 1024), 24)
     w, b = _r((576, 1024), 25, 1 / 32.0), _r((576,), 26, 0.1)
