@@ -59,7 +59,7 @@ class OpConvArgs(C.Structure):
                 ("kpad", C.c_int), ("N", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
                 ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int),
                 ("act_plane", vp), ("act_plane_lo_off", i64), ("act_alpha_exp", fp), ("act_inv_beta", fp),
-                ("act_up_filter", fp), ("act_down_filter", fp)]
+                ("act_up_filter", fp), ("act_down_filter", fp), ("geglu_plane", vp)]
 
 
 class NamedTensor(C.Structure):
@@ -89,6 +89,7 @@ _SIGS = [
     ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_flash_attention", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
+    ("alcm_layer_norm_plane", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, vp, C.c_int, vp]),
     ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_lcm_step_cfg", C.c_int, [fp, fp, fp, C.c_float, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),
     ("alcm_sincos_embedding", C.c_int, [fp, C.c_float, fp, C.c_int, C.c_int, C.c_int, fp, vp]),

@@ -128,6 +128,46 @@ int layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const 
   return 0;
 }
 
+// LayerNorm straight into an MFMA operand plane (fp16 or bf16 [rows][C]) for a conv that reads planes
+// (DiT Conv1dFeedForward input, concatDiT.py:120-125 / new_attention.py:48-74)
+template <int PREC>
+__global__ __launch_bounds__(256) void ln_plane_kernel(const float* __restrict__ x, int rows, int C, int64_t ld,
+                                                       float eps, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, u16* __restrict__ y) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ld;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c];
+  const float mean = wave_sum(s) / (float)C;
+  float v = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float d = xr[c] - mean;
+    v += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)C + eps);
+  u16* yr = y + (int64_t)row * C;
+  for (int c = lane; c < C; c += 64) {
+    const float o = (xr[c] - mean) * rstd * gamma[c] + beta[c];
+    yr[c] = PREC == PREC_F16 ? __builtin_bit_cast(u16, (_Float16)o) : __builtin_bit_cast(u16, (__bf16)o);
+  }
+}
+
+int layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, const float* gamma, const float* beta,
+                     void* plane, int prec, hipStream_t s) {
+  if (!x || !plane || !gamma || !beta || rows <= 0 || C <= 0 || (prec != PREC_F16 && prec != PREC_BF16))
+    return set_error(ALCM_E_INVALID, "layer_norm_plane: bad arguments");
+  if (prec == PREC_F16)
+    hipLaunchKernelGGL(ln_plane_kernel<PREC_F16>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, ld, eps, gamma,
+                       beta, (u16*)plane);
+  else
+    hipLaunchKernelGGL(ln_plane_kernel<PREC_BF16>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, ld, eps, gamma,
+                       beta, (u16*)plane);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 // ---------------------------------------------------------------- row softmax (in place)
 // sim.softmax(dim=-1) (new_attention.py:121) and AttnBlock1D's softmax(dim=2) (autoencoder1d.py:270).
 __global__ __launch_bounds__(256) void softmax_kernel(float* x, int rows, int n, int64_t ld) {
@@ -399,4 +439,9 @@ extern "C" int alcm_lcm_step_cfg(const float* x, const float* eps_cond, const fl
 extern "C" int alcm_sincos_embedding(const float* v, float vscale, const float* freqs, int B, int half,
                                      int cos_first, float* out, alcm_stream_t stream) {
   return alcm::sincos_embedding(v, vscale, freqs, B, half, cos_first, out, (hipStream_t)stream);
+}
+
+extern "C" int alcm_layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, const float* gamma,
+                                     const float* beta, void* plane, int prec, alcm_stream_t stream) {
+  return alcm::layer_norm_plane(x, rows, C, ld, eps, gamma, beta, plane, prec, (hipStream_t)stream);
 }

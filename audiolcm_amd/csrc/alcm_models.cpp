@@ -689,8 +689,29 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       oo.res = ur;
       ALCM_TRY(conv(s, pff, B, L, ov, a ? blk.out2 : blk.out1, uo, oo));
     }
-    ALCM_TRY(row_stats(w.u, B * L, H, H, 1e-5f, w.mean, w.rstd, s));
-    {
+    if ((pff == PREC_F16 || pff == PREC_BF16) && !std::getenv("ALCM_NO_FFN_PLANES")) {
+      // Conv1dFeedForward on operand planes and the wide-layer kernel (alcm_wconv.hip): LayerNorm -> plane,
+      // conv k9 576 -> 2x2304 with the GEGLU epilogue writing the 2304-channel plane, conv k9 2304 -> 576
+      // + bias + residual in place (non-overlapping tiles)
+      const int inner = blk.ff0.w.rows / 2;
+      u16* p2 = reinterpret_cast<u16*>(w.g);
+      u16* p1 = p2 + (size_t)B * L * inner;
+      ALCM_TRY(layer_norm_plane(w.u, B * L, H, H, 1e-5f, blk.ln3.g, blk.ln3.b, p1, pff, s));
+      alcm_opconv_args g;
+      std::memset(&g, 0, sizeof(g));
+      g.a = p1; g.a_lo_off = 0; g.B = B; g.T = L; g.C = H; g.Cp = blk.ff0.w.cpad;
+      g.ksize = D.ff_k; g.dil = 1; g.pad = D.ff_k / 2;
+      g.w = blk.ff0.w.p; g.w_lo_off = blk.ff0.w.lo; g.kpad = blk.ff0.w.kpad; g.N = blk.ff0.w.rows;
+      g.bias = blk.ff0.b; g.out_scale = 1.f; g.prec = pff; g.geglu_plane = p2;
+      ALCM_TRY(opconv(g, s));
+      std::memset(&g, 0, sizeof(g));
+      g.a = p2; g.a_lo_off = 0; g.B = B; g.T = L; g.C = inner; g.Cp = blk.ff2.w.cpad;
+      g.ksize = D.ff_k; g.dil = 1; g.pad = D.ff_k / 2;
+      g.w = blk.ff2.w.p; g.w_lo_off = blk.ff2.w.lo; g.kpad = blk.ff2.w.kpad; g.N = blk.ff2.w.rows;
+      g.bias = blk.ff2.b; g.res = w.u; g.out = w.u; g.out_scale = 1.f; g.prec = pff;
+      ALCM_TRY(opconv(g, s));
+    } else {
+      ALCM_TRY(row_stats(w.u, B * L, H, H, 1e-5f, w.mean, w.rstd, s));
       ConvOpts o;
       o.pad = D.ff_k / 2;
       o.pro = Pro{blk.ln3.g, blk.ln3.b, 0, w.mean, w.rstd, 0};

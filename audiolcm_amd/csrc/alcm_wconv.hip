@@ -18,6 +18,7 @@
 //   * XCD-aware tile order: the N tiles of one M tile (which share the input window) run on one XCD.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "alcm_common.h"
@@ -42,6 +43,7 @@ struct WConvDev {
   float out_scale;
   int accumulate;
   int tiles_per_batch, tiles_n, nwg;
+  u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
 };
@@ -262,6 +264,26 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
       __syncthreads();
       const int r0 = t0 + h * 128;
       constexpr int PER = 128 * (BN / 4) / 512;
+      if (P.gplane) {
+        // GEGLU (new_attention.py:48-55): columns (2j, 2j+1) = (value j, gate j) -> v * gelu_erf(gate)
+        const int No = P.N / 2;
+        for (int e = 0; e < PER; ++e) {
+          const int idx = tid + e * 512;
+          const int m = idx / cq, n = (idx - m * cq) * 4;
+          if (r0 + m >= P.T) continue;
+          float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+          if (P.bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
+            v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+          }
+          f32x2 y;
+          y.x = v.x * alcm_act(v.y, ACT_GELU_ERF);
+          y.y = v.z * alcm_act(v.w, ACT_GELU_ERF);
+          op_store2<PREC>(P.gplane + ((int64_t)b * P.T + r0 + m) * No + (col0 + n) / 2, 0, y);
+        }
+        __syncthreads();
+        continue;
+      }
       float4 rv[PER], pv[PER];
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
@@ -322,19 +344,21 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   const char* env = std::getenv("ALCM_WCONV");  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop
   const int var = env ? std::atoi(env) : 5;      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;
-  if (var <= 0 && !act) return 0;
+  if (var <= 0 && !act && !a.geglu_plane) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.Cp % 64 || a.ksize < 2 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
   const int BN = a.N % 192 == 0 ? 192 : (a.N % 128 == 0 ? 128 : 0);
   if (!BN) return 0;
-  if (!act && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
+  if (!act && !a.geglu_plane && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
+  if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
   WConvDev P{};
   P.a = (const u16*)a.a;
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+  P.gplane = (u16*)a.geglu_plane;
   // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 256 conv rows and emits 256 - 2 * HALO
   P.tstride = act ? WC_BM - 2 * ACT_EPI_HALO : WC_BM;
   P.tshift = act ? ACT_EPI_HALO : 0;
@@ -358,13 +382,16 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
       else go(wconv_kernel<128, PREC_BF16, V, A>);
     }
   };
-  const int V = (!act && var == 7) ? 6 : 4;
+  const int V = (!act && !a.geglu_plane && var == 7) ? 6 : 4;
   if (act) pick(std::integral_constant<int, 4>{}, std::true_type{});
   else if (V == 6) pick(std::integral_constant<int, 6>{}, std::false_type{});
   else pick(std::integral_constant<int, 4>{}, std::false_type{});
   if (tok) {
     char name[80];  // the demangled rocprofv3 name of the instantiation
     std::snprintf(name, sizeof(name), "alcm::wconv_kernel<%d, %d, %d, %s>", BN, a.prec, V, act ? "true" : "false");
+    if (std::getenv("ALCM_PROF_SHAPES"))  // diagnostics: split the statistics per layer shape
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
+                    a.ksize);
     prof_stop(tok, s, name, flops, bytes);
   }
   return 1;

@@ -378,7 +378,7 @@ def activation1d_op(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
 def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
-           act: Optional[tuple] = None, fp32_out: bool = True):
+           act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False):
     """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
 
     act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
@@ -403,6 +403,11 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
         out_scale, int(prec)
     keep = []
+    if geglu:  # GEGLU epilogue (interleaved value/gate output columns) -> operand plane (1, B, T, N/2)
+        gp = torch.empty((1, B, T, N // 2), dtype=torch.int16, device=planes.device)
+        a.out, a.geglu_plane = None, ptr(gp)
+        check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
+        return gp
     if act is not None:
         alpha, beta, fu, fd = act
         ae, ib = snake_params(alpha, beta)
@@ -433,3 +438,13 @@ def flash_attention(qkv: torch.Tensor, heads: int, prec: int) -> torch.Tensor:
     check(lib().alcm_flash_attention(ptr(qkv), ptr(out), B, L, H, heads, int(prec), stream_handle()),
           "flash_attention")
     return out
+
+
+def layer_norm_plane(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, prec: int, eps: float = 1e-5):
+    """LayerNorm over the last dim of (B, T, C) fp32 -> operand plane int16 (1, B, T, C) (fp16 or bf16 bits)."""
+    B, T, Cc = x.shape
+    x = x.contiguous()
+    y = torch.empty((1, B, T, Cc), dtype=torch.int16, device=x.device)
+    check(lib().alcm_layer_norm_plane(ptr(x), B * T, Cc, Cc, eps, ptr(gamma.contiguous()), ptr(beta.contiguous()),
+                                      ptr(y), int(prec), stream_handle()), "layer_norm_plane")
+    return y

@@ -128,6 +128,10 @@ int alcm_layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, c
                     const float* beta, const float* add, int64_t ld_add, float* y, int64_t ld_out,
                     alcm_stream_t stream);
 int alcm_softmax_rows(float* x, int rows, int n, int64_t ld, alcm_stream_t stream);
+/* LayerNorm of rows (row stride ld) written as an MFMA operand plane [rows][C] (prec PREC_F16 (2) or
+ * PREC_BF16 (0)) for alcm_opconv (the DiT feed-forward input, concatDiT.py:120-125) */
+int alcm_layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, const float* gamma,
+                          const float* beta, void* plane, int prec, alcm_stream_t stream);
 /* fused Activation1d(SnakeBeta): x,y DEVICE (b,t,c) channels-last, not in place; alpha_exp = exp(alpha),
  * inv_beta = 1/(exp(beta)+1e-9) per channel (DEVICE); up_filter/down_filter: HOST arrays of 12 taps */
 int alcm_activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st,
@@ -199,6 +203,11 @@ typedef struct alcm_opconv_args {
   const float* act_inv_beta;
   const float* act_up_filter;
   const float* act_down_filter;
+  /* optional GEGLU epilogue (new_attention.py:48-55 with value/gate rows interleaved: output columns 2j, 2j+1
+   * = value j, gate j): when geglu_plane != NULL the kernel writes (v_2j + b_2j) * gelu_erf(v_2j+1 + b_2j+1)
+   * as an operand plane [B][T][N/2] in the format of `prec` (F16 / BF16) instead of the fp32 output; needs
+   * res == NULL, out_act == 0 and the wide-layer kernel (N % 128 == 0, Cp % 64 == 0). */
+  void* geglu_plane;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 

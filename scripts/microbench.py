@@ -169,6 +169,27 @@ def bench_wconv(B=32):
                 print(f"C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line) + f" | max|diff| {diff:.2e}", flush=True)
 
 
+def bench_ffn(B=32):
+    """DiT Conv1dFeedForward convs (L = 467 tokens): fp32-operand conv_kernel (LayerNorm prologue path) vs the
+    wide-layer kernel on operand planes (GEGLU plane epilogue / residual epilogue)"""
+    L, H, inner, k = 467, 576, 2304, 9
+    x = torch.randn((B, L, H), device="cuda")
+    g = torch.randn((B, L, inner), device="cuda")
+    for name, xin, cin, cout, gl in (("ffn0", x, H, 2 * inner, True), ("ffn2", g, inner, H, False)):
+        w = torch.randn((cout, cin, k), device="cuda") / (cin * k) ** 0.5
+        b = torch.randn(cout, device="cuda") * 0.05
+        pw = K.pack_conv_weight(w)
+        pl = K.operand_planes(xin, 2)
+        tf = 2 * B * L * cin * cout * k / 1e12
+        ms0 = timeit(lambda: K.conv1d(xin, w, b, padding=k // 2, channels_last=True, packed=pw, prec=2), reps=3)
+        if gl:
+            ms1 = timeit(lambda: K.opconv(pl, cin, w, b, 1, 2, packed=pw, geglu=True), reps=3)
+        else:
+            ms1 = timeit(lambda: K.opconv(pl, cin, w, b, 1, 2, residual=x, packed=pw), reps=3)
+        print(f"{name}: conv_kernel {ms0:.3f} ms ({tf / ms0 * 1e3:.0f} TF/s) | planes+wconv {ms1:.3f} ms "
+              f"({tf / ms1 * 1e3:.0f} TF/s)", flush=True)
+
+
 def bench_tail(B=32):
     """BigVGAN tail (C = 96/48/24) conv launches as the model runs them: conv1 (dilated) + fused Activation1d
     epilogue, conv2 + residual (+ fused Activation1d): opconv_kernel (ALCM_NCONV=0) vs nconv_kernel"""
@@ -214,4 +235,4 @@ if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["amp", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
+        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()

@@ -152,6 +152,31 @@ def test_flash_attention(K, B, L, heads, dh, prec):
     assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
 
 
+@pytest.mark.parametrize("prec", [2, 0])
+def test_feedforward_on_planes(K, prec):
+    """DiT Conv1dFeedForward on operand planes: LayerNorm -> plane, conv k9 with the GEGLU plane epilogue
+    (interleaved value/gate columns), conv k9 + residual — vs fp32 F.conv1d / F.gelu."""
+    B, L, H, inner, k = 2, 300, 576, 2304, 9
+    x = _r((B, L, H), 110)
+    gam, bet = 1 + _r((H,), 111, 0.1), _r((H,), 112, 0.1)
+    w0, b0 = _r((2 * inner, H, k), 113, 1 / np.sqrt(H * k)), _r((2 * inner,), 114, 0.05)
+    w2, b2 = _r((H, inner, k), 115, 1 / np.sqrt(inner * k)), _r((H,), 116, 0.05)
+    h = F.layer_norm(x, (H,), gam, bet, 1e-5)
+    y0 = F.conv1d(h.permute(0, 2, 1), w0, b0, padding=k // 2)
+    val, gate = y0.chunk(2, dim=1)
+    gg = val * F.gelu(gate)
+    ref = (F.conv1d(gg, w2, b2, padding=k // 2) + x.permute(0, 2, 1)).permute(0, 2, 1)
+    p1 = K.layer_norm_plane(dev(x), dev(gam), dev(bet), prec)
+    dec = (lambda p: p.view(torch.float16).float()) if prec == 2 else (lambda p: p.view(torch.bfloat16).float())
+    assert rel_l2(dec(p1[0].cpu()).numpy(), h.numpy()) < (1e-3 if prec == 2 else 6e-3)
+    wi = torch.stack([w0[:inner], w0[inner:]], 1).reshape(2 * inner, H, k)   # rows (value j, gate j)
+    bi = torch.stack([b0[:inner], b0[inner:]], 1).reshape(2 * inner)
+    p2 = K.opconv(p1, H, dev(wi), dev(bi), 1, prec, geglu=True)
+    assert rel_l2(dec(p2[0].cpu()).numpy(), gg.permute(0, 2, 1).numpy()) < TOL[prec]
+    y = K.opconv(p2, inner, dev(w2), dev(b2), 1, prec, residual=dev(x)).cpu()
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+
+
 def test_linear_and_layer_norm(K):
     x = _r((3, 77, 1024), 24)
     w, b = _r((576, 1024), 25, 1 / 32.0), _r((576,), 26, 0.1)
