@@ -7,6 +7,8 @@
 
 namespace alcm {
 
+// 12-tap FIR pair of Activation1d; `up` holds 2 x the UpSample1d taps (its ratio-2 gain folded in,
+// resample.py:30: x = ratio * conv_transpose1d(...)), `dn` the LowPassFilter1d taps
 struct Taps12O {
   float up[12], dn[12];
 };
@@ -15,16 +17,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// x + h - h*cos(2*pi*r), r = x*ea_rev - rint(x*ea_rev): SnakeBeta (activations.py:62-119) with
-// h = inv_beta/2, ea_rev = exp(alpha)/pi, since sin^2(z) = 1/2 - cos(2z)/2
+// x + h - h*cos(2*pi*fract(x*ea_rev)): SnakeBeta (activations.py:62-119) with h = inv_beta/2,
+// ea_rev = exp(alpha)/pi, since sin^2(z) = 1/2 - cos(2z)/2 and v_cos_f32 takes revolutions
+// (fract: one v_fract_f32 instead of rint + sub; the argument error it adds is < 6e-8 revolutions)
 __device__ __forceinline__ f32x2 snake2(f32x2 u, f32x2 ear, f32x2 h) {
   const f32x2 z = u * ear;
-  f32x2 r;
-  r.x = z.x - rintf(z.x);
-  r.y = z.y - rintf(z.y);
   f32x2 c;
-  c.x = __builtin_amdgcn_cosf(r.x);
-  c.y = __builtin_amdgcn_cosf(r.y);
+  c.x = __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(z.x));
+  c.y = __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(z.y));
   return fma2(-h, c, u + h);
 }
 
@@ -62,7 +62,7 @@ __device__ __forceinline__ void act_run_interior(const f32x2 (&win)[R + 12], con
       const int k = 2 * kk + (q & 1);
       u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
     }
-    const f32x2 sv = snake2(u * 2.0f, ear, h);
+    const f32x2 sv = snake2(u, ear, h);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = q - 2 * r;
@@ -86,7 +86,7 @@ __device__ __forceinline__ f32x2 act_one_clamped(int j, int T, const Taps12O& f,
       xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
       u = fma2(f32x2{f.up[ku], f.up[ku]}, ld(xi), u);
     }
-    o = fma2(f32x2{f.dn[k], f.dn[k]}, snake2(u * 2.0f, ear, h), o);
+    o = fma2(f32x2{f.dn[k], f.dn[k]}, snake2(u, ear, h), o);
   }
   return o;
 }
@@ -101,19 +101,19 @@ struct ActEpiDev {
   Taps12O f;
 };
 
-constexpr int ACT_EPI_R = 8;  // output rows per work item
 constexpr int ACT_EPI_HALO = 8;  // conv tile rows computed beyond each side of the emitted rows
 
-// Activation1d of an LDS-staged fp32 tile.  tile[(t - trow0) * ots + col] holds v(b, t, c0 + col) for
+// Activation1d of an LDS-staged fp32 tile, R output rows per work item (the caller picks R so that
+// (emitted rows / R) x channel pairs fills its threads: fewer, longer runs also cut the halo recompute,
+// (2R + 10) / (2R) upsampled samples per output).  tile[(t - trow0) * ots + col] holds v(b, t, c0 + col) for
 // t in [trow0, trow0 + rows) (clamped to [0, T)); emits rows [e_lo, e_hi) for columns [0, ncol) (ncol even)
 // of batch b into the planes; channels c >= C are written as zeros (operand padding).  The tile must cover
 // [max(e_lo - 6, 0), min(e_hi + 6, T)).
-template <int PREC>
+template <int PREC, int R>
 __device__ __forceinline__ void act_epilogue_tile(const float* tile, int ots, int trow0, int e_lo, int e_hi, int T,
                                                   int ncol, int c0, int C, int b, const ActEpiDev& A, int tid,
                                                   int nthr) {
   constexpr float INV_PI = 0.318309886183790671538f;
-  constexpr int R = ACT_EPI_R;
   const int npairs = ncol >> 1;
   const int nrun = (e_hi - e_lo + R - 1) / R;
   for (int w = tid; w < npairs * nrun; w += nthr) {

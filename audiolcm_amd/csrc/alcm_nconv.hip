@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256) void nconv_kernel(const NConvDev P) {
   }
   if constexpr (ACT) {
     __syncthreads();
-    act_epilogue_tile<PREC>(ot, OTS, t0, e_lo, e_hi, P.T, P.act.Cp, 0, P.N, b, P.act, tid, 256);
+    // 240 emitted rows: R = 15 -> 16 runs x 12 pairs (C = 24) = one pass of the 256 threads
+    act_epilogue_tile<PREC, (BM == 256 ? 15 : 8)>(ot, OTS, t0, e_lo, e_hi, P.T, P.act.Cp, 0, P.N, b, P.act, tid, 256);
   }
 }
 

@@ -105,7 +105,7 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
     return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
   Taps12O f;
   for (int k = 0; k < 12; ++k) {
-    f.up[k] = up_filter[k];
+    f.up[k] = 2.0f * up_filter[k];
     f.dn[k] = down_filter[k];
   }
   const int64_t y_lo = (int64_t)B * T * Cp;
@@ -418,7 +418,9 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
       }
       __syncthreads();
     }
-    act_epilogue_tile<PREC>(ot, OTS, t0, e_lo, e_hi, P.T, P.act.Cp, 0, P.N, b, P.act, tid, 256);
+    // emitted rows BM - 16: 240 -> R = 15 (16 runs), 112 -> R = 14 (8 runs)
+    act_epilogue_tile<PREC, (BM == 256 ? 15 : (BM == 128 ? 14 : 8))>(ot, OTS, t0, e_lo, e_hi, P.T, P.act.Cp, 0, P.N, b,
+                                                                    P.act, tid, 256);
     return;
   }
   if constexpr (VEC) {
@@ -586,7 +588,7 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
     P.act.aexp = a.act_alpha_exp;
     P.act.ibeta = a.act_inv_beta;
     for (int k = 0; k < 12; ++k) {
-      P.act.f.up[k] = a.act_up_filter[k];
+      P.act.f.up[k] = 2.0f * a.act_up_filter[k];
       P.act.f.dn[k] = a.act_down_filter[k];
     }
   }

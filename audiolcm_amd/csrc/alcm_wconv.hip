@@ -239,7 +239,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
         }
         __syncthreads();
       }
-      act_epilogue_tile<PREC>(ot, OTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 512);
+      act_epilogue_tile<PREC, 15>(ot, OTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 512);
       __syncthreads();
     }
     return;
