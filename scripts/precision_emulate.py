@@ -42,6 +42,8 @@ def run(W, mel, policy, wscale=False):
     real_conv, real_convt = F.conv1d, F.conv_transpose1d
 
     def q(x, w, grp):
+        if grp not in policy and grp in ("s3", "s4", "s5"):
+            grp = "tail"  # per-stage tail groups fall back to the whole-tail policy
         a_f, w_f = policy.get(grp, ("f32", "f32"))
         w_r = scaled_f16(w) if (w_f == "f16" and wscale) else rnd(w, w_f)
         return rnd(x, a_f), w_r
@@ -62,7 +64,7 @@ def run(W, mel, policy, wscale=False):
 
     def amp(Wd, p, x, k, d):
         i = int(p.split(".")[1]) // 3
-        state["group"] = "wide" if i < 3 else "tail"
+        state["group"] = "wide" if i < 3 else f"s{i}"
         y = real_amp(Wd, p, x, k, d)
         state["group"] = "post"
         return y
@@ -97,6 +99,12 @@ def main():
             "tail bf16": {"tail": ("bf16", "bf16")},
             "pre+ups+post bf16": {k: ("bf16", "bf16") for k in ("pre", "ups", "post")},
         }
+        if len(sys.argv) > 2 and sys.argv[2] == "tail":  # per-stage weight rounding of the tail (mixed policy base)
+            base = {"wide": ("f16", "f16"), "tail": ("f16", "f32")}
+            cases = {"mixed (tail F16W2)": base}
+            for st in ("s3", "s4", "s5"):
+                cases[f"mixed + {st} F16"] = dict(base, **{st: ("f16", "f16")})
+            cases["mixed + s3,s4 F16"] = dict(base, s3=("f16", "f16"), s4=("f16", "f16"))
         for name, pol in cases.items():
             for ws in ((False, True) if any(v[1] == "f16" for v in pol.values()) else (False,)):
                 out = run(W, mel, pol, wscale=ws)
