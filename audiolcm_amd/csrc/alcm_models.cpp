@@ -109,6 +109,11 @@ struct alcm_model {
   alcm::DitW dit;
   alcm::VaeW vae;
   alcm::VocW voc;
+  // BigVGAN: the three resblocks of a stage are independent chains until their mean; they run on the
+  // caller's stream plus two auxiliary streams (created on first use, ordered by events) so the VALU / HBM
+  // bound Activation1d kernels of one chain overlap the MFMA-bound convs of another
+  hipStream_t aux[2] = {nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace alcm {
@@ -883,10 +888,17 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
 }
 
 // ------------------------------------------------------------------ BigVGAN
-struct VocWs {
-  float *x, *y, *rb, *t;
+struct VocChain {  // per-resblock scratch: running state ping-pong and the two operand-plane buffers
+  float *rb, *t;
   u16 *pl, *pl2;  // Activation1d outputs as MFMA operand planes (each 2 planes of B * T * Cp)
+};
+struct VocWs {
+  float *x, *y;
+  VocChain ch[3];
   int64_t pl_lo;
+  // legacy single-chain names (chain 0)
+  float *rb, *t;
+  u16 *pl, *pl2;
 };
 static size_t voc_elems(const VocW& G, int M) {
   size_t big = (size_t)M * G.c0;
@@ -908,10 +920,16 @@ static VocWs plan_voc(const VocW& G, Bump& bp, int B, int M) {
   VocWs w;
   w.x = bp.take<float>(e);
   w.y = bp.take<float>(e);
-  w.rb = bp.take<float>(e);
-  w.t = bp.take<float>(e);
-  w.pl = bp.take<u16>(2 * pe);
-  w.pl2 = bp.take<u16>(2 * pe);
+  for (VocChain& c : w.ch) {
+    c.rb = bp.take<float>(e);
+    c.t = bp.take<float>(e);
+    c.pl = bp.take<u16>(2 * pe);
+    c.pl2 = bp.take<u16>(2 * pe);
+  }
+  w.rb = w.ch[0].rb;
+  w.t = w.ch[0].t;
+  w.pl = w.ch[0].pl;
+  w.pl2 = w.ch[0].pl2;
   w.pl_lo = (int64_t)pe;
   return w;
 }
@@ -929,8 +947,21 @@ static int voc_prec(const alcm_model* m, int si) {
   return si < f16_upto ? PREC_F16 : PREC_F16W2;
 }
 
-static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs& w, int B, int T, int C, int prec) {
-  return activation1d_op(x, w.pl, B, T, C, round_up(C, 32), a.aexp, a.ibeta, a.fup, a.fdn, prec, s);
+static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs& w, int B, int T, int C, int prec,
+                      u16* planes = nullptr) {
+  return activation1d_op(x, planes ? planes : w.pl, B, T, C, round_up(C, 32), a.aexp, a.ibeta, a.fup, a.fdn, prec,
+                         s);
+}
+
+static bool voc_streams(alcm_model* m) {
+  if (std::getenv("ALCM_SERIAL_RESBLOCKS")) return false;  // diagnostics / A-B
+  if (!m->aux[0]) {
+    for (auto& a : m->aux)
+      if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) return false;
+    for (auto& e : m->ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+  }
+  return true;
 }
 
 // conv on the operand planes `in`; with `act` the epilogue also writes Activation1d(conv + bias (+ res)) into
@@ -997,32 +1028,45 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // writes the fp32 running state, ping-ponged between rb and y since its tiles overlap, plus planes)
     const float inv = 1.0f / (float)S.rb.size();
     const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
+    const bool conc = S.rb.size() <= 3 && voc_streams(m);
+    if (conc) {  // chains start after the upsampler wrote u
+      ALCM_HIP(hipEventRecord(m->ev[0], s));
+      for (auto a : m->aux) ALCM_HIP(hipStreamWaitEvent(a, m->ev[0], 0));
+    }
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
+      const VocChain& cb = w.ch[conc ? j : 0];
+      const hipStream_t sj = (conc && j > 0) ? m->aux[j - 1] : s;
       const float* cur = u;
-      float* nxt = rb;
+      float* nxt = cb.rb;
       for (size_t l = 0; l < A.dil.size(); ++l) {
         const bool last = l + 1 == A.dil.size();
+        // the mean over resblocks accumulates into x: the chains' last convs run in order (j-1 before j)
+        if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, m->ev[j], 0));
         if (fuse) {
-          if (l == 0) ALCM_TRY(act_planes(s, A.act[0], cur, w, B, To, S.cout, pamp));
-          ALCM_TRY(plane_conv(s, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, w.pl,
-                              &A.act[2 * l + 1], w.pl2));
+          if (l == 0) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
+          ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
+                              &A.act[2 * l + 1], cb.pl2));
           if (last) {
-            ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, x, inv, j > 0, 0, pamp, w.pl2));
+            ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, x, inv, j > 0, 0, pamp, cb.pl2));
           } else {
-            ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, nxt, 1.f, 0, 0, pamp, w.pl2, &A.act[2 * l + 2], w.pl));
+            ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, nxt, 1.f, 0, 0, pamp, cb.pl2, &A.act[2 * l + 2],
+                                cb.pl));
             cur = nxt;
-            nxt = nxt == rb ? y : rb;
+            nxt = nxt == cb.rb ? cb.t : cb.rb;
           }
-          continue;
+        } else {
+          ALCM_TRY(act_planes(sj, A.act[2 * l], cur, w, B, To, S.cout, pamp, cb.pl));
+          ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, cb.t, 1.f, 0, 0, pamp, cb.pl));
+          ALCM_TRY(act_planes(sj, A.act[2 * l + 1], cb.t, w, B, To, S.cout, pamp, cb.pl));
+          ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, last ? x : cb.rb, last ? inv : 1.f, last && j > 0, 0,
+                              pamp, cb.pl));
+          cur = cb.rb;
         }
-        ALCM_TRY(act_planes(s, A.act[2 * l], cur, w, B, To, S.cout, pamp));
-        ALCM_TRY(plane_conv(s, A.c1[l], w, B, To, A.dil[l], nullptr, y, 1.f, 0, 0, pamp));
-        ALCM_TRY(act_planes(s, A.act[2 * l + 1], y, w, B, To, S.cout, pamp));
-        ALCM_TRY(plane_conv(s, A.c2[l], w, B, To, 1, cur, last ? x : rb, last ? inv : 1.f, last && j > 0, 0, pamp));
-        cur = rb;
+        if (last && conc) ALCM_HIP(hipEventRecord(m->ev[j + 1], sj));
       }
     }
+    if (conc) ALCM_HIP(hipStreamWaitEvent(s, m->ev[S.rb.size()], 0));  // the stage output is complete
     T = To;
   }
   // activation_post -> conv_post k7 -> tanh (models.py:201-203)
@@ -1080,6 +1124,10 @@ extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, co
 
 extern "C" int alcm_model_destroy(alcm_model* m) {
   if (!m) return 0;
+  for (auto a : m->aux)
+    if (a) (void)hipStreamDestroy(a);
+  for (auto e : m->ev)
+    if (e) (void)hipEventDestroy(e);
   for (void* p : m->allocs) (void)hipFree(p);
   delete m;
   return 0;
