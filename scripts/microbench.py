@@ -195,7 +195,7 @@ def bench_tail(B=32):
     epilogue, conv2 + residual (+ fused Activation1d): opconv_kernel (ALCM_NCONV=0) vs nconv_kernel"""
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    for C, T, p in ((96, 39936, 3), (48, 79872, 3), (24, 159744, 3)):
+    for C, T, p in ((96, 39936, 2), (48, 79872, 3), (24, 159744, 3)):  # mixed-policy precisions
         x = torch.randn((B, T, C), device="cuda")
         r = torch.randn((B, T, C), device="cuda")
         a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
@@ -206,7 +206,11 @@ def bench_tail(B=32):
             pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
             line = []
             for v in os.environ.get("NCONV_VARS", "0,1").split(","):
-                os.environ["ALCM_NCONV"] = v
+                os.environ["ALCM_NCONV"] = v.split(":")[0]
+                if ":" in v:
+                    os.environ["ALCM_NCONV_NB"] = v.split(":")[1]
+                else:
+                    os.environ.pop("ALCM_NCONV_NB", None)
                 ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
                 ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
                 ms3 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))

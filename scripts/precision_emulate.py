@@ -105,6 +105,11 @@ def main():
             for st in ("s3", "s4", "s5"):
                 cases[f"mixed + {st} F16"] = dict(base, **{st: ("f16", "f16")})
             cases["mixed + s3,s4 F16"] = dict(base, s3=("f16", "f16"), s4=("f16", "f16"))
+            base2 = dict(base, s3=("f16", "f16"))
+            cases["mixed(s3 F16) + ups F16W2"] = dict(base2, ups=("f16", "f32"))
+            cases["mixed(s3 F16) + ups F16"] = dict(base2, ups=("f16", "f16"))
+            cases["mixed(s3 F16) + pre F16W2"] = dict(base2, pre=("f16", "f32"))
+            cases["mixed(s3 F16) + ups bf16"] = dict(base2, ups=("bf16", "bf16"))
         for name, pol in cases.items():
             for ws in ((False, True) if any(v[1] == "f16" for v in pol.values()) else (False,)):
                 out = run(W, mel, pol, wscale=ws)
