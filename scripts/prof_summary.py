@@ -52,8 +52,9 @@ def main():
     json.dump(out, open(os.path.join(dst, "kernels.json"), "w"), indent=1)
     with open(os.path.join(dst, "SUMMARY.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary ({os.path.basename(dst)})\n\n"
-                 "Source: `scripts/profile_bench.sh` (kernel-trace --stats over `bench.py --steps 2 --warmup 1`, "
-                 "then separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes over one step).  HBM read = "
+                 "Source: `scripts/gpu_profile.sh` (rocprofv3 kernel-trace --stats over `bench.py --steps 1 --warmup 1` "
+                 "with ALCM_SERIAL_RESBLOCKS=1 — the bench's headline pass plus its roofline pass, so every launch "
+                 "appears twice per step — then separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes).  HBM read = "
                  "2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE, averaged per launch.\n\n"
                  "| kernel | calls | avg us | % time | HBM read MB/launch | HBM write MB/launch | HBM GB/s |\n"
                  "|---|---|---|---|---|---|---|\n")
