@@ -37,8 +37,9 @@ __device__ __forceinline__ u16 fa_cvt(float v) {
 }
 
 template <int PREC>
-__global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict__ qkv, float* __restrict__ O, int L,
-                                                         int H, int nh, int dh, float scale) {
+__global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict__ qkv, float* __restrict__ O,
+                                                         u16* __restrict__ Op, int L, int H, int nh, int dh,
+                                                         float scale) {
   __shared__ __attribute__((aligned(16))) u16 Ks[FA_KT * FA_KS];
   __shared__ __attribute__((aligned(16))) u16 Vt[FA_DV * FA_VS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -158,19 +159,29 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict
   const int q = q0 + cq;
   if (q >= L) return;
   const float inv = 1.0f / l;
-  float* orow = O + ((int64_t)b * L + q) * H + h * dh;
+  const int64_t ob = ((int64_t)b * L + q) * H + h * dh;
+  if (Op) {  // operand plane for the to_out projection (the same rounding its GEMM would apply)
+#pragma unroll
+    for (int db = 0; db < 5; ++db)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = 16 * db + 4 * g + r;
+        if (d < dh) Op[ob + d] = fa_cvt<PREC>(o[db][r] * inv);
+      }
+    return;
+  }
 #pragma unroll
   for (int db = 0; db < 5; ++db)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int d = 16 * db + 4 * g + r;
-      if (d < dh) orow[d] = o[db][r] * inv;
+      if (d < dh) O[ob + d] = o[db][r] * inv;
     }
 }
 
 // qkv: (B, L, 3H) fp32 rows [q | k | v], head h at columns h*dh; O: (B, L, H) fp32
-int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s) {
-  if (!qkv || !O || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
+int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s, void* o_plane) {
+  if (!qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
   const int dh = H / nh;
   if (dh > 72 || dh % 4 || H % 4) return set_error(ALCM_E_INVALID, "flash_attention: head dim must be <= 72, % 4");
   if (prec != PREC_F16 && prec != PREC_BF16) return set_error(ALCM_E_INVALID, "flash_attention: F16 or BF16 only");
@@ -178,8 +189,10 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
   const dim3 grid((L + FA_Q - 1) / FA_Q, B * nh);
   const float scale = 1.0f / std::sqrt((float)dh);
   void* tok = prof_start(s);
-  if (prec == PREC_F16) hipLaunchKernelGGL(flash_attn_kernel<PREC_F16>, grid, dim3(256), 0, s, qkv, O, L, H, nh, dh, scale);
-  else hipLaunchKernelGGL(flash_attn_kernel<PREC_BF16>, grid, dim3(256), 0, s, qkv, O, L, H, nh, dh, scale);
+  if (prec == PREC_F16)
+    hipLaunchKernelGGL(flash_attn_kernel<PREC_F16>, grid, dim3(256), 0, s, qkv, O, (u16*)o_plane, L, H, nh, dh, scale);
+  else
+    hipLaunchKernelGGL(flash_attn_kernel<PREC_BF16>, grid, dim3(256), 0, s, qkv, O, (u16*)o_plane, L, H, nh, dh, scale);
   if (tok) {
     char name[64];
     std::snprintf(name, sizeof(name), "alcm::flash_attn_kernel<%d>", prec);

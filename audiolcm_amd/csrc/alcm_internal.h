@@ -48,7 +48,9 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
 int nconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
-int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s);
+// o_plane != nullptr: write the output as an fp16 / bf16 operand plane [B][L][H] instead of fp32 O
+int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s,
+                    void* o_plane = nullptr);
 // whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
 bool opconv_act_supported(int prec, int N, int Cp_in);
 // actepi: const ActEpiDev* (alcm_actepi.h) or nullptr

@@ -683,7 +683,31 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       ALCM_TRY(conv(s, split, B, L, hv, blk.proj_in, uo, o));
     }
     // BasicTransformerBlock (concatDiT.py:120-125)
-    for (int a = 0; a < 2; ++a) {
+    const bool planes = (pff == PREC_F16 || pff == PREC_BF16) && (H / D.heads) <= 72 && (H / D.heads) % 4 == 0 &&
+                        !std::getenv("ALCM_NO_ATTN_PLANES");
+    for (int a = 0; a < 2 && planes; ++a) {
+      // attention sub-block on operand planes: LayerNorm -> plane, fused q/k/v projection (k = 1 on the
+      // wide-layer kernel), flash attention writing the to_out operand plane, to_out + bias + residual in place
+      const NormW& ln = a ? blk.ln2 : blk.ln1;
+      const ConvW& wq = a ? blk.qkv2 : blk.qkv1;
+      const ConvW& wo = a ? blk.out2 : blk.out1;
+      u16* pln = reinterpret_cast<u16*>(w.g);  // w.g is free until the feed-forward below
+      u16* opl = pln + (size_t)B * L * H;
+      ALCM_TRY(layer_norm_plane(w.u, B * L, H, H, 1e-5f, ln.g, ln.b, pln, pff, s));
+      alcm_opconv_args g;
+      std::memset(&g, 0, sizeof(g));
+      g.a = pln; g.B = B; g.T = L; g.C = H; g.Cp = wq.w.cpad; g.ksize = 1; g.dil = 1; g.pad = 0;
+      g.w = wq.w.p; g.w_lo_off = wq.w.lo; g.kpad = wq.w.kpad; g.N = wq.w.rows;
+      g.bias = wq.b; g.out = w.qkv; g.out_scale = 1.f; g.prec = pff;
+      ALCM_TRY(opconv(g, s));
+      ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, H, D.heads, pff, s, opl));
+      std::memset(&g, 0, sizeof(g));
+      g.a = opl; g.B = B; g.T = L; g.C = H; g.Cp = wo.w.cpad; g.ksize = 1; g.dil = 1; g.pad = 0;
+      g.w = wo.w.p; g.w_lo_off = wo.w.lo; g.kpad = wo.w.kpad; g.N = wo.w.rows;
+      g.bias = wo.b; g.res = w.u; g.out = w.u; g.out_scale = 1.f; g.prec = pff;
+      ALCM_TRY(opconv(g, s));
+    }
+    for (int a = 0; a < 2 && !planes; ++a) {
       const NormW& ln = a ? blk.ln2 : blk.ln1;
       ALCM_TRY(row_stats(w.u, B * L, H, H, 1e-5f, w.mean, w.rstd, s));
       ConvOpts oq;

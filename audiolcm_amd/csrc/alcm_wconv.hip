@@ -346,7 +346,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   const bool act = actepi != nullptr;
   if (var <= 0 && !act && !a.geglu_plane) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  if (a.out_act || a.Cp % 64 || a.ksize < 2 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
+  if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
   const int BN = a.N % 192 == 0 ? 192 : (a.N % 128 == 0 ? 128 : 0);
   if (!BN) return 0;
   if (!act && !a.geglu_plane && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
