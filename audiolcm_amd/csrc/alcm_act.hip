@@ -1,0 +1,128 @@
+// Activation1d -> MFMA operand planes, LDS-cooperative form (alias_free_torch/act.py:23-27:
+// UpSample1d x2 -> SnakeBeta -> DownSample1d; resample.py:10-48, activations.py:62-119).
+//
+// The Activation1d arithmetic is VALU-bound (two 12-tap FIRs and a cos per upsampled sample).  The
+// per-thread form (act_op_kernel) recomputes the 10 upsampled samples that overlap neighbouring runs
+// (26 upsampled samples per 8 outputs).  Here a workgroup owns a tile of AC_TT output rows x 32 channels of
+// one batch:
+//   phase 1: every upsampled + SnakeBeta sample of the tile (2 per output + 10 halo) is computed exactly
+//            once, by threads (channel pair, segment of consecutive samples), into LDS;
+//   phase 2: threads (channel pair, run of 8 outputs) apply the 12-tap down filter from LDS and write the
+//            operand planes.
+// Replicate padding (UpSample1d pad 5 on x, DownSample1d pad 5/6 on the upsampled signal) is applied by
+// computing the sample at the clamped index, so phase 2 needs no edge cases.  ~19 VALU issue slots per
+// element instead of ~30.
+#include <cstdio>
+#include <cstdlib>
+
+#include "alcm_common.h"
+#include "alcm_internal.h"
+#include "alcm_actepi.h"
+
+namespace alcm {
+
+constexpr int AC_TT = 128;                 // output rows per tile
+constexpr int AC_NP = 16;                  // channel pairs per tile (32 channels)
+constexpr int AC_SEG = 18;                 // upsampled samples per phase-1 thread (even: static FIR indexing)
+constexpr int AC_NU = 16 * AC_SEG;         // upsampled samples staged per channel (>= 2 * AC_TT + 11)
+constexpr int AC_RS = AC_NP + 1;           // LDS sample-row stride (f32x2): conflict-free phase-2 row reads
+
+template <int PREC>
+__global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__ x, u16* __restrict__ y,
+                                                       int64_t y_lo, int T, int C, int Cp,
+                                                       const float* __restrict__ aexp,
+                                                       const float* __restrict__ ibeta, const Taps12O f,
+                                                       int tiles_t, int tiles_c) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  __shared__ __attribute__((aligned(16))) f32x2 sv[AC_NU * AC_RS];  // [m - m0][pair]
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int ct = bid % tiles_c;
+  bid /= tiles_c;
+  const int tt = bid % tiles_t;
+  const int b = bid / tiles_t;
+  const int t0 = tt * AC_TT, c0 = ct * 2 * AC_NP;
+  const int p = tid & (AC_NP - 1);
+  const int c = c0 + 2 * p;
+  const bool live = c < C;  // pairs at or beyond C: operand padding (zeros)
+  const float* xb = x + ((int64_t)b * T) * C + (live ? c : 0);
+  const f32x2 ear = live ? f32x2{aexp[c], aexp[c + 1]} * INV_PI : f32x2{0.f, 0.f};
+  const f32x2 h = live ? f32x2{ibeta[c], ibeta[c + 1]} * 0.5f : f32x2{0.f, 0.f};
+  const int m0 = 2 * t0 - 6;  // sample index 0 of the tile (even); output j reads m = 2j - 5 .. 2j + 6
+
+  // ---- phase 1: upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
+  //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
+  if (live) {
+    const int seg = tid >> 4;
+    const int mb = m0 + seg * AC_SEG;
+    const int xlo = mb / 2 - 3;  // sample mb + q reads x rows xlo + (q + 5 - ku) / 2 + 3 - 3
+    if (mb >= 0 && mb + AC_SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1) {
+      f32x2 win[15];
+#pragma unroll
+      for (int i = 0; i < 15; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(xlo + i) * C);
+#pragma unroll
+      for (int q = 0; q < AC_SEG; ++q) {
+        f32x2 u = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int ku = 2 * kk + ((q & 1) ? 0 : 1);
+          u = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u);
+        }
+        sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
+      }
+    } else {
+      for (int q = 0; q < AC_SEG; ++q) {
+        int m = mb + q;
+        m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+        f32x2 u = f32x2{0.f, 0.f};
+        for (int kk = 0; kk < 6; ++kk) {
+          const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+          int xi = (m + 5 - ku) / 2;
+          xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+          u = fma2(f32x2{f.up[ku], f.up[ku]}, *reinterpret_cast<const f32x2*>(xb + (int64_t)xi * C), u);
+        }
+        sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: outputs j0 .. j0 + 7 of pair p: o[j] = sum_k dn[k] * sv[2j + k - 5 - m0]
+  const int run = tid >> 4;
+  const int j0 = t0 + run * 8;
+  if (j0 >= T) return;
+  u16* yb = y + ((int64_t)b * T) * Cp + c;
+  const int jn = min(8, T - j0);
+  if (!live) {
+    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, f32x2{0.f, 0.f});
+    return;
+  }
+  const f32x2* sp = sv + (2 * (j0 - t0) + 1) * AC_RS + p;
+  f32x2 s[26];
+#pragma unroll
+  for (int i = 0; i < 26; ++i) s[i] = sp[i * AC_RS];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    f32x2 o = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) o = fma2(f32x2{f.dn[k], f.dn[k]}, s[2 * r + k], o);
+    if (r < jn) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o);
+  }
+}
+
+int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
+             const Taps12O& f, int prec, hipStream_t s) {
+  const int tiles_t = (T + AC_TT - 1) / AC_TT, tiles_c = Cp / (2 * AC_NP);
+  const int64_t nwg = (int64_t)B * tiles_t * tiles_c;
+  if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
+  const int64_t y_lo = (int64_t)B * T * Cp;
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
+                       tiles_t, tiles_c);
+  };
+  if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT>);
+  else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16>);
+  else launch(act_coop_kernel<PREC_F16>);
+  return 0;
+}
+
+}  // namespace alcm

@@ -23,6 +23,9 @@
 
 namespace alcm {
 
+int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
+             const Taps12O& f, int prec, hipStream_t s);
+
 // sin(x)^2: Cody-Waite quadrant reduction + minimax sin/cos on |r| <= pi/4 (~1 ulp, branch-free)
 __device__ __forceinline__ float op_sin_sq(float x) {
   const float k = rintf(x * 0.63661977236758134f);
@@ -110,6 +113,18 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   }
   const int64_t y_lo = (int64_t)B * T * Cp;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
+  if (!std::getenv("ALCM_ACT_V1")) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
+    void* tok = prof_start(s);
+    ALCM_TRY(act_coop(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
+    if (tok) {
+      char name[64];
+      std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>", prec == PREC_F16W2 ? PREC_F16 : prec);
+      const double e = (double)B * T;
+      prof_stop(tok, s, name, 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
+    }
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
   void* tok = prof_start(s);
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
