@@ -36,6 +36,9 @@ int layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const 
 int softmax_rows(float* x, int rows, int n, int64_t ld, hipStream_t s);
 int layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, const float* gamma, const float* beta,
                      void* plane, int prec, hipStream_t s);
+// plane[b][t'][c] = (silu?)(x[b][t'/up][c] * scale[b][c] + shift[b][c]) (scale == nullptr: identity)
+int affine_plane(const float* x, int B, int T, int C, int up, const float* scale, const float* shift, int silu,
+                 void* plane, int prec, hipStream_t s);
 int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st, const float* alpha_exp,
                  const float* inv_beta, const float* up_filter, const float* down_filter, hipStream_t s);
 int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,

@@ -168,6 +168,56 @@ int layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, con
   return 0;
 }
 
+// GroupNorm affine (+ swish) straight into an MFMA operand plane, optionally nearest-upsampled along t:
+// plane[b][t'][c] = act(x[b][t'/up][c] * scale[b][c] + shift[b][c]).  The VAE decoder's
+// norm -> nonlinearity -> conv k3 (ResnetBlock1D, autoencoder1d.py:212-235) and Upsample1D's
+// interpolate(nearest) -> conv (autoencoder1d.py:291-295) then run on the wide-layer conv kernel.
+// One workgroup per output row, 4 channels per thread (C % 4 == 0, contiguous (B, T, C) input).
+template <int PREC, bool SILU>
+__global__ __launch_bounds__(256) void affine_plane_kernel(const float* __restrict__ x, int T, int C, int up,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, u16* __restrict__ y) {
+  const int row = blockIdx.x;  // b * (T * up) + t'
+  const int To = T * up;
+  const int b = row / To, to = row - b * To;
+  const float4* xr = reinterpret_cast<const float4*>(x + ((int64_t)b * T + to / up) * C);
+  const float4* sc = scale ? reinterpret_cast<const float4*>(scale + (int64_t)b * C) : nullptr;
+  const float4* sh = scale ? reinterpret_cast<const float4*>(shift + (int64_t)b * C) : nullptr;
+  uint2* yr = reinterpret_cast<uint2*>(y + (int64_t)row * C);
+  auto cv = [](float o) -> uint32_t {
+    if (SILU) o = o / (1.0f + __expf(-o));
+    return PREC == PREC_F16 ? (uint32_t)__builtin_bit_cast(u16, (_Float16)o)
+                            : (uint32_t)__builtin_bit_cast(u16, (__bf16)o);
+  };
+  for (int c = threadIdx.x; c < C / 4; c += 256) {
+    float4 v = xr[c];
+    if (sc) {
+      const float4 a = sc[c], h = sh[c];
+      v.x = v.x * a.x + h.x; v.y = v.y * a.y + h.y; v.z = v.z * a.z + h.z; v.w = v.w * a.w + h.w;
+    }
+    yr[c] = make_uint2(cv(v.x) | (cv(v.y) << 16), cv(v.z) | (cv(v.w) << 16));
+  }
+}
+
+int affine_plane(const float* x, int B, int T, int C, int up, const float* scale, const float* shift, int silu,
+                 void* plane, int prec, hipStream_t s) {
+  if (!x || !plane || B <= 0 || T <= 0 || C <= 0 || C % 4 || up < 1 || (scale && !shift) ||
+      (prec != PREC_F16 && prec != PREC_BF16) || (((uintptr_t)x) & 15) || (((uintptr_t)plane) & 7) ||
+      (scale && ((((uintptr_t)scale) & 15) || (((uintptr_t)shift) & 15))) || (int64_t)B * T * up >= (1ll << 31))
+    return set_error(ALCM_E_INVALID, "affine_plane: bad arguments");
+  const dim3 grid((unsigned)(B * T * up)), blk(256);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, blk, 0, s, x, T, C, up, scale, shift, (u16*)plane); };
+  if (prec == PREC_F16) {
+    if (silu) go(affine_plane_kernel<PREC_F16, true>);
+    else go(affine_plane_kernel<PREC_F16, false>);
+  } else {
+    if (silu) go(affine_plane_kernel<PREC_BF16, true>);
+    else go(affine_plane_kernel<PREC_BF16, false>);
+  }
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 // ---------------------------------------------------------------- row softmax (in place)
 // sim.softmax(dim=-1) (new_attention.py:121) and AttnBlock1D's softmax(dim=2) (autoencoder1d.py:270).
 __global__ __launch_bounds__(256) void softmax_kernel(float* x, int rows, int n, int64_t ld) {

@@ -770,7 +770,24 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
 // ------------------------------------------------------------------ VAE decoder
 struct VaeWs {
   float *a, *b, *c, *d, *qkv, *S, *gsc, *gsh, *pqs, *pqh;
+  u16* pl;  // operand plane of the k3 conv inputs (F16 / BF16 layers)
 };
+// the VAE's k3 convs read operand planes on the wide-layer kernel unless ALCM_NO_VAE_PLANES is set
+static bool vae_planes(int pk3) {
+  return (pk3 == PREC_F16 || pk3 == PREC_BF16) && !std::getenv("ALCM_NO_VAE_PLANES");
+}
+// conv k3 (same length) on an operand plane: out = conv(plane) + bias (+ res); out may alias res
+static int plane_conv3(hipStream_t s, int prec, int B, int T, int C, const u16* plane, const ConvW& cw,
+                       const float* res, float* out) {
+  if (cw.w.cpad != C || cw.w.cin != C) return set_error(ALCM_E_INVALID, "plane_conv3: plane width != packed Cin");
+  alcm_opconv_args g;
+  std::memset(&g, 0, sizeof(g));
+  g.a = plane; g.a_lo_off = 0; g.B = B; g.T = T; g.C = C; g.Cp = cw.w.cpad;
+  g.ksize = cw.w.taps; g.dil = 1; g.pad = cw.w.taps / 2;
+  g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
+  g.bias = cw.b; g.res = res; g.out = out; g.out_scale = 1.f; g.prec = prec;
+  return opconv(g, s);
+}
 static VaeWs plan_vae(const VaeW& V, Bump& bp, int B, int T) {
   // largest channels x time of any activation on the decode path
   const int nl = (int)V.mult.size();
@@ -797,6 +814,7 @@ static VaeWs plan_vae(const VaeW& V, Bump& bp, int B, int T) {
   w.gsh = bp.take<float>((size_t)B * maxc);
   w.pqs = bp.take<float>((size_t)V.z_ch);
   w.pqh = bp.take<float>((size_t)V.z_ch);
+  w.pl = bp.take<u16>((size_t)B * big);
   return w;
 }
 
@@ -804,6 +822,20 @@ static VaeWs plan_vae(const VaeW& V, Bump& bp, int B, int T) {
 static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& r, const float* x, float* tmp,
                    float* sc, float* out, VaeWs& w) {
   ALCM_TRY(group_norm_affine(x, B, T, r.cin, (int64_t)T * r.cin, r.cin, 32, 1e-6f, r.n1.g, r.n1.b, w.gsc, w.gsh, s));
+  if (vae_planes(pk3)) {
+    // GN affine + swish -> plane, conv1 on the wide-layer kernel; again for conv2 with bias + residual
+    ALCM_TRY(affine_plane(x, B, T, r.cin, 1, w.gsc, w.gsh, 1, w.pl, pk3, s));
+    ALCM_TRY(plane_conv3(s, pk3, B, T, r.cin, w.pl, r.c1, nullptr, tmp));
+    ALCM_TRY(group_norm_affine(tmp, B, T, r.cout, (int64_t)T * r.cout, r.cout, 32, 1e-6f, r.n2.g, r.n2.b, w.gsc,
+                               w.gsh, s));
+    const float* resid = x;
+    if (r.has_nin) {
+      ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.nin, ocl(sc, T, r.cout), ConvOpts{}));
+      resid = sc;
+    }
+    ALCM_TRY(affine_plane(tmp, B, T, r.cout, 1, w.gsc, w.gsh, 1, w.pl, pk3, s));
+    return plane_conv3(s, pk3, B, T, r.cout, w.pl, r.c2, resid, out);
+  }
   ConvOpts o1;
   o1.pad = 1;
   o1.pro = Pro{w.gsc, w.gsh, r.cin, nullptr, nullptr, ACT_SILU};
@@ -894,7 +926,13 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
       }
       C = r.cout;
     }
-    if (V.up[lvl].w.p) {
+    if (V.up[lvl].w.p && vae_planes(pk3)) {
+      // Upsample1D: nearest x2 written as a duplicated-row plane, conv k3 on the wide-layer kernel
+      ALCM_TRY(affine_plane(h, B, Tc, C, 2, nullptr, nullptr, 0, w.pl, pk3, s));
+      ALCM_TRY(plane_conv3(s, pk3, B, 2 * Tc, C, w.pl, V.up[lvl], nullptr, spare));
+      std::swap(h, spare);
+      Tc *= 2;
+    } else if (V.up[lvl].w.p) {
       // Upsample1D: nearest x2 folded into the conv's input index (autoencoder1d.py:291-295)
       ConvOpts o;
       o.pad = 1;

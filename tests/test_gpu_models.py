@@ -65,6 +65,20 @@ def test_vae_decode_mixed(M):
     assert rel_l2(mel, g["mel"]) < 1e-3
 
 
+def test_vae_decode_mixed_batched_planes(M):
+    # B=4 x T=312 rows reach the wide-layer kernel (>= 1024 rows) for the plane-input k3 convs;
+    # every clip must match the fp32 golden within the mixed-policy mel bound (1e-3)
+    g = golden("vae_T312.npz")
+    z = torch.from_numpy(g["z"]).repeat(4, 1, 1).cuda()
+    M["vae"].set_split("mixed")
+    try:
+        mel = M["vae"].decode(z).cpu().numpy()
+    finally:
+        M["vae"].set_split(True)
+    for i in range(4):
+        assert rel_l2(mel[i:i + 1], g["mel"]) < 1e-3
+
+
 def test_vae_decode_bf16(M):
     g = golden("vae_T312.npz")
     M["vae"].set_split(False)
