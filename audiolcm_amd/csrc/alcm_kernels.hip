@@ -39,21 +39,18 @@ __global__ __launch_bounds__(256) void gn_affine_kernel(const float* __restrict_
   const int cg = C / groups;
   const float* base = x + (int64_t)b * sb + g * cg;
   const int64_t n = (int64_t)cg * T;
-  double s = 0.0;
+  // one pass over the group: fp64 sum and sum of squares (53-bit accumulation of fp32 inputs, so
+  // E[x^2] - mean^2 keeps fp32-level accuracy for any mean/std ratio these activations reach)
+  double s = 0.0, q = 0.0;
   for (int64_t e = threadIdx.x; e < n; e += 256) {
     uint32_t t, c;
     cgdiv.divmod((uint32_t)e, t, c);
-    s += (double)base[(int64_t)t * st + c];
+    const double x1 = (double)base[(int64_t)t * st + c];
+    s += x1;
+    q += x1 * x1;
   }
   const double mean = block_sum(s, sh) / (double)n;
-  double v = 0.0;
-  for (int64_t e = threadIdx.x; e < n; e += 256) {
-    uint32_t t, c;
-    cgdiv.divmod((uint32_t)e, t, c);
-    const double d = (double)base[(int64_t)t * st + c] - mean;
-    v += d * d;
-  }
-  const double var = block_sum(v, sh) / (double)n;
+  const double var = fmax(block_sum(q, sh) / (double)n - mean * mean, 0.0);
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float fmean = (float)mean;
   for (int c = threadIdx.x; c < cg; c += 256) {
