@@ -44,15 +44,6 @@ class GemmArgs(C.Structure):
                 ("disable_window", C.c_int), ("tile_n", C.c_int)]
 
 
-class AmpArgs(C.Structure):
-    _fields_ = [("x", fp), ("B", C.c_int), ("T", C.c_int), ("Cin", C.c_int), ("act", C.c_int),
-                ("alpha_exp", fp), ("inv_beta", fp), ("up_filter", fp), ("down_filter", fp), ("w", vp),
-                ("w_lo_off", i64), ("kpad", C.c_int), ("Cout", C.c_int), ("ksize", C.c_int), ("dil", C.c_int),
-                ("pad", C.c_int), ("bias", fp), ("res", fp), ("out", fp), ("out_act", C.c_int),
-                ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int),
-                ("seg_tiles", C.c_int)]
-
-
 class OpConvArgs(C.Structure):
     _fields_ = [("a", vp), ("a_lo_off", i64), ("B", C.c_int), ("T", C.c_int), ("C", C.c_int), ("Cp", C.c_int),
                 ("ksize", C.c_int), ("dil", C.c_int), ("pad", C.c_int), ("w", vp), ("w_lo_off", i64),
@@ -85,7 +76,6 @@ _SIGS = [
     ("alcm_layer_norm", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, fp, i64, fp, i64, vp]),
     ("alcm_softmax_rows", C.c_int, [fp, C.c_int, C.c_int, i64, vp]),
     ("alcm_activation1d", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, i64, i64, fp, fp, fp, fp, vp]),
-    ("alcm_amp_conv", C.c_int, [C.POINTER(AmpArgs), vp]),
     ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_flash_attention", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
@@ -99,6 +89,8 @@ _SIGS = [
     ("alcm_model_weight_bytes", C.c_size_t, [vp]),
     ("alcm_model_set_split", C.c_int, [vp, C.c_int]),
     ("alcm_model_set_precision", C.c_int, [vp, C.c_int]),
+    ("alcm_model_set_resblock_streams", C.c_int, [vp, C.c_int]),
+    ("alcm_reload_knobs", C.c_int, []),
     ("alcm_dit_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_dit_embed_context", C.c_int, [vp, fp, C.c_int, fp, vp, C.c_size_t, vp]),
     ("alcm_dit_forward", C.c_int, [vp, fp, vp, fp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
@@ -161,6 +153,11 @@ def ptr(t) -> Optional[int]:
     if t is None:
         return None
     return int(t.data_ptr())
+
+
+def reload_knobs() -> None:
+    """Re-read the ALCM_* diagnostic switches (the library reads them once at load)."""
+    check(lib().alcm_reload_knobs(), "alcm_reload_knobs")
 
 
 PEAK_BF16_FLOPS = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)

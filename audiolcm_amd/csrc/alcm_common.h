@@ -29,12 +29,12 @@ struct FastDiv {
   }
 };
 
-// MFMA operand precision (alcm_gemm_args.prec / alcm_amp_args.prec):
+// MFMA operand precision (alcm_gemm_args.prec / alcm_opconv_args.prec):
 //   PREC_BF16  one bf16 MFMA (operands rounded to bf16)
 //   PREC_SPLIT bf16x3: hi*hi + hi*lo + lo*hi, ~fp32 accuracy
 //   PREC_F16   one fp16 MFMA (operands rounded to fp16, 8x finer than bf16)
-//   PREC_F16W2 fp16 activation x fp16 hi+lo weight, 2 MFMAs (only the activation is rounded; fused
-//              BigVGAN narrow-stage kernel only)
+//   PREC_F16W2 fp16 activation x fp16 hi+lo weight, 2 MFMAs (only the activation is rounded; BigVGAN
+//              narrow-stage operand-plane convs)
 enum AlcmPrec : int { PREC_BF16 = 0, PREC_SPLIT = 1, PREC_F16 = 2, PREC_F16W2 = 3 };
 
 // 16x16x32 MFMA step on 16-byte operand fragments held as bf16x8 (fp16 bits for PREC_F16).

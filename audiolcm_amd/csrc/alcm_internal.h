@@ -44,7 +44,6 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
 int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
-int amp_conv(const alcm_amp_args& a, hipStream_t s);
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
@@ -59,6 +58,26 @@ bool opconv_act_supported(int prec, int N, int Cp_in);
 // actepi: const ActEpiDev* (alcm_actepi.h) or nullptr
 int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s);
+
+// diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
+struct Knobs {
+  int wconv = 5;                 // ALCM_WCONV: 0 = never the wide-layer kernel, 7 = setprio K loop
+  int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width
+  int nconv_nb = 0;              // ALCM_NCONV_NB: narrow-conv ring depth / tile variant
+  int act_rows = 8;              // ALCM_ACT_ROWS: rows per thread of the per-thread Activation1d kernel
+  bool act_v1 = false;           // ALCM_ACT_V1: per-thread Activation1d kernel instead of the cooperative one
+  int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
+  bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION
+  bool wide_act_fusion = false;  // ALCM_WIDE_ACT_FUSION
+  bool no_flash = false;         // ALCM_NO_FLASH
+  bool no_attn_planes = false;   // ALCM_NO_ATTN_PLANES
+  bool no_ffn_planes = false;    // ALCM_NO_FFN_PLANES
+  bool no_vae_planes = false;    // ALCM_NO_VAE_PLANES
+  bool tail_f16w2_all = false;   // ALCM_TAIL_F16W2_ALL
+  bool serial_resblocks = false; // ALCM_SERIAL_RESBLOCKS: default of alcm_model_set_resblock_streams
+  bool prof_shapes = false;      // ALCM_PROF_SHAPES: split profile rows per layer shape
+};
+const Knobs& knobs();
 
 bool prof_enabled();
 void* prof_start(hipStream_t s);

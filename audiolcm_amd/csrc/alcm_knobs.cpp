@@ -1,0 +1,47 @@
+// Diagnostic / A-B switches (ALCM_* environment variables), read once when the library is loaded and
+// again only on alcm_reload_knobs(): no launch path calls getenv.
+#include <cstdlib>
+
+#include "alcm_internal.h"
+
+namespace alcm {
+
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+static bool env_set(const char* name) {
+  const char* v = std::getenv(name);
+  return v && *v;
+}
+
+static Knobs read_knobs() {
+  Knobs k;
+  k.wconv = env_int("ALCM_WCONV", 5);
+  k.nconv = env_int("ALCM_NCONV", -1);
+  k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
+  k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;
+  k.act_v1 = env_set("ALCM_ACT_V1");
+  k.opconv_tile = env_int("ALCM_OPCONV_TILE", 0);
+  k.no_act_fusion = env_set("ALCM_NO_ACT_FUSION");
+  k.wide_act_fusion = env_set("ALCM_WIDE_ACT_FUSION");
+  k.no_flash = env_set("ALCM_NO_FLASH");
+  k.no_attn_planes = env_set("ALCM_NO_ATTN_PLANES");
+  k.no_ffn_planes = env_set("ALCM_NO_FFN_PLANES");
+  k.no_vae_planes = env_set("ALCM_NO_VAE_PLANES");
+  k.tail_f16w2_all = env_set("ALCM_TAIL_F16W2_ALL");
+  k.serial_resblocks = env_set("ALCM_SERIAL_RESBLOCKS");
+  k.prof_shapes = env_set("ALCM_PROF_SHAPES");
+  return k;
+}
+
+static Knobs g_knobs = read_knobs();
+
+const Knobs& knobs() { return g_knobs; }
+
+}  // namespace alcm
+
+extern "C" int alcm_reload_knobs(void) {
+  alcm::g_knobs = alcm::read_knobs();
+  return 0;
+}

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -110,10 +111,18 @@ struct alcm_model {
   alcm::VaeW vae;
   alcm::VocW voc;
   // BigVGAN: the three resblocks of a stage are independent chains until their mean; they run on the
-  // caller's stream plus two auxiliary streams (created on first use, ordered by events) so the VALU / HBM
-  // bound Activation1d kernels of one chain overlap the MFMA-bound convs of another
-  hipStream_t aux[2] = {nullptr, nullptr};
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // caller's stream plus two auxiliary streams ordered by events, so the VALU / HBM bound Activation1d
+  // kernels of one chain overlap the MFMA-bound convs of another.  The auxiliary streams and events belong
+  // to the CALLER's stream (created on its first call, kept until destroy): concurrent calls on one handle
+  // from different caller streams fork and join on disjoint resources, so they never order against (or
+  // race on) each other's chains.
+  struct AuxSet {
+    hipStream_t s[2] = {nullptr, nullptr};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  };
+  std::mutex aux_mu;
+  std::map<hipStream_t, AuxSet> aux;
+  bool resblock_streams = true;  // alcm_model_set_resblock_streams (default: !ALCM_SERIAL_RESBLOCKS)
 };
 
 namespace alcm {
@@ -570,7 +579,7 @@ static DitWs plan_dit(const DitW& D, Bump& bp, int B, int T) {
 static int dit_attention(hipStream_t s, int split, const DitW& D, int B, int L, const float* qkv, float* S, float* O) {
   const int H = D.hidden, nh = D.heads, dh = H / nh, Lp = round_up(L, 8);
   // single-rounding policies: fused kernel, scores never leave the chip (alcm_attn.hip)
-  if ((split == PREC_F16 || split == PREC_BF16) && dh <= 72 && dh % 4 == 0 && !std::getenv("ALCM_NO_FLASH"))
+  if ((split == PREC_F16 || split == PREC_BF16) && dh <= 72 && dh % 4 == 0 && !knobs().no_flash)
     return flash_attention(qkv, O, B, L, H, nh, split, s);
   alcm_gemm_args g;
   std::memset(&g, 0, sizeof(g));
@@ -684,7 +693,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
     }
     // BasicTransformerBlock (concatDiT.py:120-125)
     const bool planes = (pff == PREC_F16 || pff == PREC_BF16) && (H / D.heads) <= 72 && (H / D.heads) % 4 == 0 &&
-                        !std::getenv("ALCM_NO_ATTN_PLANES");
+                        !knobs().no_attn_planes;
     for (int a = 0; a < 2 && planes; ++a) {
       // attention sub-block on operand planes: LayerNorm -> plane, fused q/k/v projection (k = 1 on the
       // wide-layer kernel), flash attention writing the to_out operand plane, to_out + bias + residual in place
@@ -718,7 +727,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       oo.res = ur;
       ALCM_TRY(conv(s, pff, B, L, ov, a ? blk.out2 : blk.out1, uo, oo));
     }
-    if ((pff == PREC_F16 || pff == PREC_BF16) && !std::getenv("ALCM_NO_FFN_PLANES")) {
+    if ((pff == PREC_F16 || pff == PREC_BF16) && !knobs().no_ffn_planes) {
       // Conv1dFeedForward on operand planes and the wide-layer kernel (alcm_wconv.hip): LayerNorm -> plane,
       // conv k9 576 -> 2x2304 with the GEGLU epilogue writing the 2304-channel plane, conv k9 2304 -> 576
       // + bias + residual in place (non-overlapping tiles)
@@ -774,7 +783,7 @@ struct VaeWs {
 };
 // the VAE's k3 convs read operand planes on the wide-layer kernel unless ALCM_NO_VAE_PLANES is set
 static bool vae_planes(int pk3) {
-  return (pk3 == PREC_F16 || pk3 == PREC_BF16) && !std::getenv("ALCM_NO_VAE_PLANES");
+  return (pk3 == PREC_F16 || pk3 == PREC_BF16) && !knobs().no_vae_planes;
 }
 // conv k3 (same length) on an operand plane: out = conv(plane) + bias (+ res); out may alias res
 static int plane_conv3(hipStream_t s, int prec, int B, int T, int C, const u16* plane, const ConvW& cw,
@@ -1005,7 +1014,7 @@ static int voc_prec(const alcm_model* m, int si) {
   if (m->policy == ALCM_POLICY_SPLIT) return PREC_SPLIT;
   // stage 3 (C = 96, the costliest tail stage) tolerates fp16 weights: +1e-5 waveform rel-L2 emulated,
   // vs +2.5e-4 (stage 4) and +4.3e-4 (stage 5) (scripts/precision_emulate.py 96 tail)
-  const int f16_upto = std::getenv("ALCM_TAIL_F16W2_ALL") ? 3 : 4;  // diagnostics / A-B
+  const int f16_upto = knobs().tail_f16w2_all ? 3 : 4;  // diagnostics / A-B
   return si < f16_upto ? PREC_F16 : PREC_F16W2;
 }
 
@@ -1015,15 +1024,24 @@ static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs&
                          s);
 }
 
-static bool voc_streams(alcm_model* m) {
-  if (std::getenv("ALCM_SERIAL_RESBLOCKS")) return false;  // diagnostics / A-B
-  if (!m->aux[0]) {
-    for (auto& a : m->aux)
-      if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) return false;
-    for (auto& e : m->ev)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+// the auxiliary resblock streams / events of caller stream s (nullptr: run the chains serially on s)
+static const alcm_model::AuxSet* voc_streams(alcm_model* m, hipStream_t s) {
+  if (!m->resblock_streams) return nullptr;
+  std::lock_guard<std::mutex> lk(m->aux_mu);
+  auto it = m->aux.find(s);
+  if (it != m->aux.end()) return &it->second;
+  alcm_model::AuxSet a;
+  bool ok = true;
+  for (auto& x : a.s) ok = ok && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : a.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    for (auto x : a.s)
+      if (x) (void)hipStreamDestroy(x);
+    for (auto e : a.ev)
+      if (e) (void)hipEventDestroy(e);
+    return nullptr;
   }
-  return true;
+  return &(m->aux[s] = a);
 }
 
 // conv on the operand planes `in`; with `act` the epilogue also writes Activation1d(conv + bias (+ res)) into
@@ -1090,21 +1108,22 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // writes the fp32 running state, ping-ponged between rb and y since its tiles overlap, plus planes)
     const float inv = 1.0f / (float)S.rb.size();
     const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
-    const bool conc = S.rb.size() <= 3 && voc_streams(m);
+    const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
+    const bool conc = ax != nullptr;
     if (conc) {  // chains start after the upsampler wrote u
-      ALCM_HIP(hipEventRecord(m->ev[0], s));
-      for (auto a : m->aux) ALCM_HIP(hipStreamWaitEvent(a, m->ev[0], 0));
+      ALCM_HIP(hipEventRecord(ax->ev[0], s));
+      for (auto a : ax->s) ALCM_HIP(hipStreamWaitEvent(a, ax->ev[0], 0));
     }
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
       const VocChain& cb = w.ch[conc ? j : 0];
-      const hipStream_t sj = (conc && j > 0) ? m->aux[j - 1] : s;
+      const hipStream_t sj = (conc && j > 0) ? ax->s[j - 1] : s;
       const float* cur = u;
       float* nxt = cb.rb;
       for (size_t l = 0; l < A.dil.size(); ++l) {
         const bool last = l + 1 == A.dil.size();
         // the mean over resblocks accumulates into x: the chains' last convs run in order (j-1 before j)
-        if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, m->ev[j], 0));
+        if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, ax->ev[j], 0));
         if (fuse) {
           if (l == 0) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
@@ -1125,10 +1144,10 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
                               pamp, cb.pl));
           cur = cb.rb;
         }
-        if (last && conc) ALCM_HIP(hipEventRecord(m->ev[j + 1], sj));
+        if (last && conc) ALCM_HIP(hipEventRecord(ax->ev[j + 1], sj));
       }
     }
-    if (conc) ALCM_HIP(hipStreamWaitEvent(s, m->ev[S.rb.size()], 0));  // the stage output is complete
+    if (conc) ALCM_HIP(hipStreamWaitEvent(s, ax->ev[S.rb.size()], 0));  // the stage output is complete
     T = To;
   }
   // activation_post -> conv_post k7 -> tanh (models.py:201-203)
@@ -1166,6 +1185,7 @@ extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, co
     return set_error(ALCM_E_INVALID, "model_create: unknown precision policy");
   }
   m->policy = policy;
+  m->resblock_streams = !knobs().serial_resblocks;
   try {
     Ingest I(m, tensors, n_tensors);
     if (kind == ALCM_MODEL_DIT) build_dit(I, iconfig, n_iconfig);
@@ -1186,10 +1206,12 @@ extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, co
 
 extern "C" int alcm_model_destroy(alcm_model* m) {
   if (!m) return 0;
-  for (auto a : m->aux)
-    if (a) (void)hipStreamDestroy(a);
-  for (auto e : m->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& kv : m->aux) {
+    for (auto a : kv.second.s)
+      if (a) (void)hipStreamDestroy(a);
+    for (auto e : kv.second.ev)
+      if (e) (void)hipEventDestroy(e);
+  }
   for (void* p : m->allocs) (void)hipFree(p);
   delete m;
   return 0;
@@ -1207,6 +1229,12 @@ extern "C" int alcm_model_set_precision(alcm_model* m, int policy) {
   if (!m) return set_error(ALCM_E_INVALID, "null model");
   if (policy < ALCM_POLICY_BF16 || policy > ALCM_POLICY_MIXED) return set_error(ALCM_E_INVALID, "unknown policy");
   m->policy = policy;
+  return 0;
+}
+
+extern "C" int alcm_model_set_resblock_streams(alcm_model* m, int concurrent) {
+  if (!m) return set_error(ALCM_E_INVALID, "null model");
+  m->resblock_streams = concurrent != 0;
   return 0;
 }
 

@@ -223,13 +223,13 @@ __global__ __launch_bounds__(256) void nconv_kernel(const NConvDev P) {
 // (k-1)d <= 64, no output activation.  Returns 1 when it launched.
 int nconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
-  const char* env = std::getenv("ALCM_NCONV");  // diagnostics / A-B: ALCM_NCONV=0 uses opconv_kernel
-  if (env && std::atoi(env) == 0) return 0;
+  const int nck = knobs().nconv;  // diagnostics / A-B: ALCM_NCONV=0 uses opconv_kernel
+  if (nck == 0) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_F16W2 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.N > 96 || a.N % 4 || (a.ksize - 1) * a.dil > NC_HALO) return 0;
   // measured (scripts/microbench.py tail): faster than opconv_kernel at C = 24 only (C = 48 / 96 pad or
   // lose occupancy); ALCM_NCONV=2 forces it for every narrow shape
-  if (a.Cp != 32 && !(env && std::atoi(env) == 2)) return 0;
+  if (a.Cp != 32 && nck != 2) return 0;
   if (a.Cp != 32 && a.Cp != 64 && a.Cp != 96) return 0;
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
@@ -246,8 +246,8 @@ int nconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   int BM, BN, NB;
   // diagnostics / A-B (ALCM_NCONV_NB set): C = 24 ring depth 8 instead of 4 when it is "8"; C = 48 / 96 take
   // 128-row tiles with 3 / 2 ring buffers (3 workgroups per CU) — measured equal to opconv_kernel there
-  const char* nbe = std::getenv("ALCM_NCONV_NB");
-  const int nb32 = (nbe && std::atoi(nbe) == 8) ? 8 : 4;  // 4: 36 KB LDS -> 4 workgroups/CU (measured -12%)
+  const bool nbe = knobs().nconv_nb != 0;
+  const int nb32 = knobs().nconv_nb == 8 ? 8 : 4;  // 4: 36 KB LDS -> 4 workgroups/CU (measured -12%)
   if (a.N <= 32 && a.Cp == 32) BM = 256, BN = 32, NB = nb32;
   else if (a.N <= 64 && a.Cp == 64) BM = nbe ? 128 : 256, BN = 64, NB = nbe ? 3 : 4;
   else if (a.N <= 96 && a.Cp == 96) BM = 128, BN = 96, NB = nbe ? 2 : 3;

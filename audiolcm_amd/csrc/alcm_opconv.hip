@@ -100,8 +100,7 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   if (C % 2) return set_error(ALCM_E_INVALID, "activation1d_op: C must be even");
   if (prec < PREC_BF16 || prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "activation1d_op: bad prec");
   if ((((uintptr_t)x) & 7) || (((uintptr_t)y) & 3)) return set_error(ALCM_E_INVALID, "activation1d_op: alignment");
-  const char* rs = std::getenv("ALCM_ACT_ROWS");  // diagnostics: rows per thread (8 or 16)
-  const int R = (rs && std::atoi(rs) == 16) ? 16 : 8;
+  const int R = knobs().act_rows;  // diagnostics: rows per thread (8 or 16)
   const int runs = (T + R - 1) / R;
   const int64_t total = (int64_t)B * runs * (Cp / 2);
   if (total >= (1ll << 31) || (int64_t)B * T * Cp >= (1ll << 40))
@@ -113,7 +112,7 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   }
   const int64_t y_lo = (int64_t)B * T * Cp;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-  if (!std::getenv("ALCM_ACT_V1")) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
+  if (!knobs().act_v1) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
     void* tok = prof_start(s);
     ALCM_TRY(act_coop(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
     if (tok) {
@@ -558,18 +557,17 @@ static int launch_opconv(const OpConvDev& P, int B, int prec, bool act, double f
 // narrow-layer tile variant (diagnostics / A-B): ALCM_OPCONV_TILE=0 default, 1 = twice the rows per tile,
 // 2 = twice the rows and two taps per K step
 static int tile_variant(int prec) {
-  const char* e = std::getenv("ALCM_OPCONV_TILE");
-  return (e && prec != PREC_SPLIT) ? std::atoi(e) : 0;  // the split operands need the default tiles' LDS
+  return prec != PREC_SPLIT ? knobs().opconv_tile : 0;  // the split operands need the default tiles' LDS
 }
 
 bool opconv_act_supported(int prec, int N, int Cp_in) {
-  if (std::getenv("ALCM_NO_ACT_FUSION")) return false;  // diagnostics / A-B
+  if (knobs().no_act_fusion) return false;  // diagnostics / A-B
   if (N % 4 || N <= 0) return false;
   if (N <= 96) return true;  // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%
   // wide layers (wconv, one 512-thread workgroup per CU): the activation's VALU work in the epilogue is
   // serialised with the MFMA K loop and measured slower than the standalone act_op kernel,
   // so it is opt-in (ALCM_WIDE_ACT_FUSION=1) for A/B runs
-  if (!std::getenv("ALCM_WIDE_ACT_FUSION")) return false;
+  if (!knobs().wide_act_fusion) return false;
   return (prec == PREC_F16 || prec == PREC_BF16) && Cp_in % 64 == 0 && (N % 192 == 0 || N % 128 == 0);
 }
 

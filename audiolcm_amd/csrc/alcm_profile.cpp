@@ -6,6 +6,7 @@
 // keys use the demangled names rocprofv3 prints, so the two can be compared directly.
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -22,6 +23,7 @@ static bool g_on = false;
 static double g_pf = 2.5e15, g_pb = 8.0e12;
 static std::vector<ProfRec> g_recs;
 static std::vector<hipEvent_t> g_pool;
+static std::mutex g_mu;  // launches may come from several host threads while profiling
 
 static hipEvent_t take_event() {
   if (!g_pool.empty()) {
@@ -38,6 +40,7 @@ bool prof_enabled() { return g_on; }
 
 void* prof_start(hipStream_t s) {
   if (!g_on) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
   hipEvent_t e = take_event();
   (void)hipEventRecord(e, s);
   return (void*)e;
@@ -45,6 +48,7 @@ void* prof_start(hipStream_t s) {
 
 void prof_stop(void* tok, hipStream_t s, const std::string& name, double flops, double bytes) {
   if (!g_on || !tok) return;
+  std::lock_guard<std::mutex> lk(g_mu);
   hipEvent_t e1 = take_event();
   (void)hipEventRecord(e1, s);
   g_recs.push_back(ProfRec{name, flops, bytes, (hipEvent_t)tok, e1});
@@ -55,6 +59,7 @@ void prof_stop(void* tok, hipStream_t s, const std::string& name, double flops, 
 using namespace alcm;
 
 extern "C" int alcm_profile_begin(double peak_flops, double peak_bytes_per_s) {
+  std::lock_guard<std::mutex> lk(g_mu);
   if (peak_flops > 0) g_pf = peak_flops;
   if (peak_bytes_per_s > 0) g_pb = peak_bytes_per_s;
   for (auto& r : g_recs) {
@@ -67,6 +72,7 @@ extern "C" int alcm_profile_begin(double peak_flops, double peak_bytes_per_s) {
 }
 
 extern "C" int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_entries) {
+  std::lock_guard<std::mutex> lk(g_mu);
   g_on = false;
   struct Agg {
     int64_t n = 0;

@@ -341,8 +341,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
 // no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
-  const char* env = std::getenv("ALCM_WCONV");  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop
-  const int var = env ? std::atoi(env) : 5;      // default: plain K loop + LDS-staged epilogue (measured best)
+  const int var = knobs().wconv;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;
   if (var <= 0 && !act && !a.geglu_plane) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
@@ -389,7 +388,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   if (tok) {
     char name[80];  // the demangled rocprofv3 name of the instantiation
     std::snprintf(name, sizeof(name), "alcm::wconv_kernel<%d, %d, %d, %s>", BN, a.prec, V, act ? "true" : "false");
-    if (std::getenv("ALCM_PROF_SHAPES"))  // diagnostics: split the statistics per layer shape
+    if (knobs().prof_shapes)  // diagnostics: split the statistics per layer shape
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
     prof_stop(tok, s, name, flops, bytes);

@@ -310,39 +310,6 @@ def sincos_embedding(v: torch.Tensor, freqs: torch.Tensor, scale: float, cos_fir
     return out
 
 
-def amp_conv(x_cl: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int, padding: int,
-             act: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-             residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
-             accumulate_into: Optional[torch.Tensor] = None, split: bool = True,
-             prec: Optional[int] = None, seg_tiles: int = 0) -> torch.Tensor:
-    """Fused conv_{k,d}(Activation1d(x)) on channels-last (B, T, C) for C in {24, 48, 96}.
-
-    act = (alpha, beta, up_filter, down_filter) of the SnakeBeta Activation1d (None: no activation)."""
-    B, T, Cin = x_cl.shape
-    x_cl = x_cl.contiguous()
-    pw = pack_conv_weight(w)
-    a = _hip.AmpArgs()
-    a.x, a.B, a.T, a.Cin = ptr(x_cl), B, T, Cin
-    keep = []
-    if act is not None:
-        ae, ib = snake_params(act[0], act[1])
-        ae, ib = ae.contiguous(), ib.contiguous()
-        fu = act[2].detach().reshape(-1).float().cpu().contiguous()
-        fd = act[3].detach().reshape(-1).float().cpu().contiguous()
-        keep += [ae, ib, fu, fd]
-        a.act, a.alpha_exp, a.inv_beta, a.up_filter, a.down_filter = 1, ptr(ae), ptr(ib), fu.data_ptr(), fd.data_ptr()
-    a.w, a.w_lo_off, a.kpad, a.Cout, a.ksize, a.dil, a.pad = ptr(pw.data), pw.lo_off, pw.kpad, pw.rows, pw.taps, \
-        dilation, padding
-    a.bias = ptr(bias)
-    a.res = ptr(residual.contiguous()) if residual is not None else None
-    out = accumulate_into if accumulate_into is not None else torch.empty((B, T, pw.rows), device=x_cl.device)
-    a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
-        out_scale, _prec(split, prec)
-    a.seg_tiles = seg_tiles
-    check(lib().alcm_amp_conv(C.byref(a), stream_handle()), "amp_conv")
-    return out
-
-
 def operand_planes(x_cl: torch.Tensor, prec: int, Cp: Optional[int] = None) -> torch.Tensor:
     """(B, T, C) fp32 -> MFMA operand planes int16 (NP, B, T, Cp) as alcm_activation1d_op writes them
     (without the activation): fp16 for PREC_F16/F16W2, bf16 for PREC_BF16, bf16 hi/lo for PREC_SPLIT."""

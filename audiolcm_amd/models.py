@@ -91,6 +91,11 @@ class _HipModel:
 
     set_precision = set_split
 
+    def set_resblock_streams(self, concurrent: bool):
+        """BigVGAN: resblock chains on auxiliary streams (True) or serially on the caller's stream (False)."""
+        self._need()
+        check(lib().alcm_model_set_resblock_streams(self._handle, int(bool(concurrent))))
+
     @property
     def loaded(self) -> bool:
         return bool(self._handle)
@@ -103,9 +108,13 @@ class _HipModel:
             raise RuntimeError(f"{type(self).__name__}: weights not loaded (call load_state_dict)")
 
     def _workspace(self, key: tuple, nbytes: int, device) -> torch.Tensor:
+        """Caller-side workspace, one per (call kind, shape, stream): calls issued concurrently on different
+        streams never share one (the C-ABI concurrency contract, include/audiolcm_hip.h)."""
+        key = key + (stream_handle(),)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < nbytes:
-            self._ws.clear()
+            for k in [k for k in self._ws if k[-1] == key[-1]]:
+                del self._ws[k]
             ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
             self._ws[key] = ws
         return ws

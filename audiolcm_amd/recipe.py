@@ -250,7 +250,11 @@ def kaiser_sinc_filter1d(cutoff: float, half_width: float, kernel_size: int) -> 
     """Windowed-sinc low-pass used by Activation1d up/down sampling.
 
     Follows alias_free_torch/filter.py:28-57 (Kaiser beta from the stop-band
-    attenuation, even-length half-sample time grid, unit DC gain)."""
+    attenuation, even-length half-sample time grid, unit DC gain).  That reference
+    file is itself adapted from the `julius` package (MIT, Alexandre Défossez,
+    ``julius/lowpass.py``) by the alias-free-torch project (Apache-2.0, junjun3518);
+    the formula is the standard Kaiser window design (Kaiser & Schafer 1980,
+    Oppenheim & Schafer eq. 7.62-7.63) and is restated here with that attribution."""
     even = kernel_size % 2 == 0
     half = kernel_size // 2
     delta_f = 4 * half_width

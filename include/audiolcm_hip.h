@@ -10,7 +10,16 @@
  *     fp32, contiguous; sizes are explicit;
  *   - work is enqueued on the caller's hipStream_t (torch.cuda.current_stream());
  *     no call allocates device memory except the *_create loaders, no call
- *     synchronises the host, calls are re-entrant across streams;
+ *     synchronises the host;
+ *   - concurrency: calls on one model handle from different host threads and/or
+ *     different caller streams may overlap, provided each concurrent call has its
+ *     own workspace and output buffers.  The handle's packed weights are read-only
+ *     after *_create; the only per-handle mutable state is the set of auxiliary
+ *     streams/events alcm_bigvgan_forward forks its resblock chains onto, which is
+ *     kept per CALLER stream (created under a lock on that stream's first call), so
+ *     concurrent calls never share an event.  alcm_model_set_precision /
+ *     alcm_model_set_resblock_streams must not race with calls on the same handle.
+ *     Two calls on the SAME caller stream are ordered by that stream;
  *   - no torch types cross the boundary.
  *
  * Reference interfaces replaced (paths under the reference checkout):
@@ -57,7 +66,7 @@ int alcm_check_device(int dev);
  *   ALCM_PREC_BF16  (0) one v_mfma_f32_16x16x32_bf16 (operands rounded to bf16)
  *   ALCM_PREC_SPLIT (1) 3-term bf16 split (hi*hi + hi*lo + lo*hi): fp32-level accuracy, 3x the MFMA work
  *   ALCM_PREC_F16   (2) one v_mfma_f32_16x16x32_f16 (operands rounded to fp16)
- *   ALCM_PREC_F16W2 (3) fp16 activation x fp16 hi+lo weight, 2 MFMAs (alcm_amp_conv only) */
+ *   ALCM_PREC_F16W2 (3) fp16 activation x fp16 hi+lo weight, 2 MFMAs (alcm_opconv only) */
 enum { ALCM_PREC_BF16 = 0, ALCM_PREC_SPLIT = 1, ALCM_PREC_F16 = 2, ALCM_PREC_F16W2 = 3 };
 enum { ALCM_OPND_ACT = 0, ALCM_OPND_ACT_T = 1, ALCM_OPND_WEIGHT = 2 };
 
@@ -137,31 +146,6 @@ int alcm_layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps
 int alcm_activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int64_t st,
                       const float* alpha_exp, const float* inv_beta, const float* up_filter,
                       const float* down_filter, alcm_stream_t stream);
-
-/* fused BigVGAN narrow-stage layer (C = 24/48/96): y = conv_{k,dil}(Activation1d(x)) + bias, then
- * optional out_act (ACT_TANH for conv_post), + res, * out_scale, + out (accumulate).
- * x (B,T,Cin), res/out (B,T,Cout) channels-last DEVICE; w packed as alcm_pack_conv_weight
- * (cpad = Cin); act=0 skips the activation; filters are HOST arrays of 12 taps. */
-typedef struct alcm_amp_args {
-  const float* x;
-  int B, T, Cin;
-  int act;
-  const float* alpha_exp;
-  const float* inv_beta;
-  const float* up_filter;
-  const float* down_filter;
-  const void* w;
-  int64_t w_lo_off;
-  int kpad, Cout, ksize, dil, pad;
-  const float* bias;
-  const float* res;
-  float* out;
-  int out_act, accumulate;
-  float out_scale;
-  int prec;      /* ALCM_PREC_* */
-  int seg_tiles; /* 0: automatic; > 0 forces the output sub-tiles streamed per workgroup (tests) */
-} alcm_amp_args;
-int alcm_amp_conv(const alcm_amp_args* args, alcm_stream_t stream);
 
 /* ---------------------------------------------------------------- operand-format AMPBlock path
  * (vocoder/bigvgan/models.py:72-81 as Activation1d -> conv, alcm_opconv.hip)
@@ -260,6 +244,12 @@ int alcm_model_set_split(alcm_model* m, int split);
  * bf16x3 elsewhere.  alcm_model_set_split(m, s) == set_precision(m, s ? SPLIT : BF16). */
 enum { ALCM_POLICY_BF16 = 0, ALCM_POLICY_SPLIT = 1, ALCM_POLICY_MIXED = 2 };
 int alcm_model_set_precision(alcm_model* m, int policy);
+/* BigVGAN: run the three resblock chains of a stage concurrently on auxiliary streams forked from the caller's
+ * stream (1, the default unless ALCM_SERIAL_RESBLOCKS is set at load) or serially on the caller's stream (0:
+ * per-kernel timing, bench.py's roofline pass) */
+int alcm_model_set_resblock_streams(alcm_model* m, int concurrent);
+/* re-read the ALCM_* diagnostic environment switches (they are read once at library load) */
+int alcm_reload_knobs(void);
 
 /* DiT.  x (B,C_lat,T) NCT, t (B,) int64, ctx (B,154,1024), w_emb (B,256) -> eps (B,C_lat,T) NCT.
  * cemb_cache: (B,154,hidden) device buffer filled by alcm_dit_embed_context (step-invariant, hoisted). */

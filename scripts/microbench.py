@@ -2,7 +2,7 @@
 """Per-kernel microbenchmarks on BigVGAN / DiT shapes (B=32), timed with torch CUDA events.
 
 Used to A/B kernel variants in one process and as the target of rocprofv3 PMC passes:
-    python scripts/microbench.py amp        # fused Activation1d+conv, C=24/48/96
+    python scripts/microbench.py op         # Activation1d -> operand planes + plane conv per BigVGAN stage
     python scripts/microbench.py conv       # window conv, BigVGAN stage 0-2 / VAE / DiT FFN shapes
     python scripts/microbench.py act        # standalone Activation1d
 """
@@ -28,24 +28,6 @@ def timeit(fn, reps=5):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
-
-
-def bench_amp(B=32):
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    for C, T in ((24, 159744), (48, 79872), (96, 39936)):
-        x = torch.randn((B, T, C), device="cuda")
-        r = torch.randn((B, T, C), device="cuda")
-        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
-        for k, d in ((11, 5), (3, 1)):
-            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
-            bias = torch.randn(C, device="cuda") * 0.05
-            for prec, act in ((1, True), (3, True), (2, True), (1, False)):
-                ms = timeit(lambda: K.amp_conv(x, w, bias, d, (k * d - d) // 2,
-                                               act=(a, bt, f, f) if act else None, residual=r, prec=prec))
-                gb = B * T * C * 4 * 3 / 1e9
-                tf = 2 * B * T * C * C * k / 1e12
-                print(f"amp C={C:3d} k={k:2d} d={d} prec={prec} act={int(act)}: {ms:7.3f} ms "
-                      f"{gb / ms:6.2f} TB/s {tf / ms * 1e3:7.1f} TF/s", flush=True)
 
 
 def bench_conv(B=32):
@@ -75,18 +57,6 @@ def bench_act(B=32):
         print(f"act1d C={C} T={T}: {ms:.3f} ms {B * T * C * 8 / 1e9 / ms:.2f} TB/s")
 
 
-def bench_amp_one(B=32, C=24, k=3, d=1, reps=5):
-    """single configuration (target for rocprofv3 --pmc passes)"""
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    T = 3833856 // C
-    x = torch.randn((B, T, C), device="cuda")
-    r = torch.randn((B, T, C), device="cuda")
-    a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
-    w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
-    ms = timeit(lambda: K.amp_conv(x, w, None, d, (k * d - d) // 2, act=(a, bt, f, f), residual=r), reps=reps)
-    print(f"amp1 C={C} k={k} d={d}: {ms:.3f} ms {B * T * C * 12 / 1e9 / ms:.2f} TB/s")
-
-
 def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
     """single window-conv configuration (target for rocprofv3 --pmc passes)"""
     x = torch.randn((B, T, C), device="cuda")
@@ -95,27 +65,6 @@ def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
     ms = timeit(lambda: K.conv1d(x, w, None, padding=(k * d - d) // 2, dilation=d, split=split, channels_last=True,
                                  packed=pw), reps=3)
     print(f"conv1 C={C} k={k}: {ms:.3f} ms {2 * B * T * C * C * k / 1e9 / ms:.1f} TF/s algorithmic")
-
-
-def bench_amp_ablate(B=32):
-    """phase costs of the fused narrow-stage kernel: ALCM_AMP_ABLATE bit0 = no activation, bit1 = no K loop,
-    bit2 = no epilogue (timing diagnostics; results are wrong under ablation)"""
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    for C, T in ((24, 159744), (48, 79872), (96, 39936)):
-        x = torch.randn((B, T, C), device="cuda")
-        r = torch.randn((B, T, C), device="cuda")
-        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
-        for k, d in ((11, 5), (3, 1)):
-            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
-            res = []
-            for ab in (0, 1, 2, 4, 3, 6, 5, 7):
-                os.environ["ALCM_AMP_ABLATE"] = str(ab)
-                res.append(timeit(lambda: K.amp_conv(x, w, None, d, (k * d - d) // 2, act=(a, bt, f, f), residual=r,
-                                                      split=True)))
-            os.environ.pop("ALCM_AMP_ABLATE")
-            print(f"amp C={C:3d} k={k:2d} split act res | full {res[0]:.3f} -act {res[1]:.3f} -mfma {res[2]:.3f} "
-                  f"-epi {res[3]:.3f} | only-epi {res[4]:.3f} only-act {res[5]:.3f} only-mfma {res[6]:.3f} "
-                  f"none {res[7]:.3f} ms", flush=True)
 
 
 def bench_op(B=32):
@@ -132,6 +81,7 @@ def bench_op(B=32):
             gb = B * T * (C * 4 + cp * 2 * npl) / 1e9
             for rows in ("8", "16"):
                 os.environ["ALCM_ACT_ROWS"] = rows
+                _hip.reload_knobs()
                 ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p))
                 print(f"act_op C={C:3d} prec={p} rows={rows}: {ms:7.3f} ms {gb / ms:6.2f} TB/s", flush=True)
             pl = K.activation1d_op(x, a, bt, f, f, p)
@@ -161,10 +111,12 @@ def bench_wconv(B=32):
                 outs, line = [], []
                 for wc in os.environ.get("WCONV_VARS", "0,1").split(","):
                     os.environ["ALCM_WCONV"] = wc
+                    _hip.reload_knobs()
                     ms = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
                     outs.append(K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
                     line.append(f"wconv={wc} {ms:7.3f} ms {tf / ms * 1e3:7.1f} TF/s")
                 os.environ.pop("ALCM_WCONV")
+                _hip.reload_knobs()
                 diff = max(float((outs[0] - o).abs().max()) for o in outs[1:])
                 print(f"C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line) + f" | max|diff| {diff:.2e}", flush=True)
 
@@ -207,15 +159,19 @@ def bench_tail(B=32):
             line = []
             for v in os.environ.get("NCONV_VARS", "0,1").split(","):
                 os.environ["ALCM_NCONV"] = v.split(":")[0]
+                _hip.reload_knobs()
                 if ":" in v:
                     os.environ["ALCM_NCONV_NB"] = v.split(":")[1]
+                    _hip.reload_knobs()
                 else:
                     os.environ.pop("ALCM_NCONV_NB", None)
+                    _hip.reload_knobs()
                 ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
                 ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
                 ms3 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
                 line.append(f"v{v}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
             os.environ.pop("ALCM_NCONV")
+            _hip.reload_knobs()
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
 
 
@@ -237,6 +193,6 @@ def bench_op1(B=32):
 
 if __name__ == "__main__":
     _hip.require_device(0)
-    which = sys.argv[1:] or ["amp", "conv", "act"]
+    which = sys.argv[1:] or ["op", "conv", "act"]
     for w in which:
-        {"amp": bench_amp, "ablate": bench_amp_ablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "amp1": bench_amp_one, "conv1": bench_conv_one}[w]()
+        {"op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
