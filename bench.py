@@ -50,28 +50,54 @@ def parse():
                          "everywhere (fp32 parity); bf16 = one bf16 MFMA everywhere (misses the parity bar)")
     ap.add_argument("--also-other-mode", type=int, default=1, help="N=1: also time the other precision policies")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-clips", type=int, default=2)
+    ap.add_argument("--cpu-clips", type=int, default=1, help="clips per timed CPU run (median of 3 runs)")
+    ap.add_argument("--extra-configs", type=int, default=1,
+                    help="N=1: also time BASELINE configs[3] (C4: B=64, 4 steps + CFG) and configs[4] (C5: B=16, "
+                         "30 s decode) and report them beside the headline")
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(clips: int, latent_len: int, lcm_steps: int):
-    """The oracle (fp32 PyTorch-CPU restatement of the reference path) on a bounded sample."""
+    """The oracle (fp32 PyTorch-CPU restatement of the reference path, pinned to the reference's fixtures) on a
+    bounded sample, per BASELINE.md §4: all the cores this process may use, one warm-up, median of 3 runs."""
+    import statistics
     from audiolcm_amd import recipe
     from oracle import alcm_oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cores = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")  # the GPU box sets the job's CPU share here (16 per GPU)
+    threads = max(1, min(cores, int(share))) if share and share.isdigit() else cores
     torch.set_num_threads(threads)
     Wd, Wv, Wg = recipe.dit_state(0), recipe.vae_state(0), recipe.bigvgan_state(0)
     ctx = recipe.synthetic_context(clips)
     xT, noise = recipe.prompt_noise(range(clips), lcm_steps, 20, latent_len)
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        for i in range(clips):  # per clip, as the reference API (InferAPI.py:159-163)
-            O.generate(Wd, Wv, Wg, ctx[i:i + 1], xT[i:i + 1], noise[:, i:i + 1], S=lcm_steps)
-    dt = time.perf_counter() - t0
+
+    def run():
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for i in range(clips):  # per clip, as the reference API (InferAPI.py:159-163)
+                O.generate(Wd, Wv, Wg, ctx[i:i + 1], xT[i:i + 1], noise[:, i:i + 1], S=lcm_steps)
+        return time.perf_counter() - t0
+    run()  # warm-up
+    times = [run() for _ in range(3)]
+    dt = statistics.median(times)
     audio = clips * latent_len * 2 * HOP / SR
-    return dict(value=round(audio / dt, 4), unit="audio-s/s", cores=threads, kind="port",
+    return dict(value=round(audio / dt, 4), unit="audio-s/s", cores=threads, kind="port", cpu_model=cpu_model(),
+                affinity_cores=cores,
                 sample=f"{clips} clip(s) x {lcm_steps} LCM steps, {audio / clips:.3f} s each, batch 1 per clip, "
-                       f"fp32 torch-CPU oracle, {dt:.1f} s wall")
+                       f"fp32 torch-CPU oracle; median of 3 timed runs after 1 warm-up "
+                       f"({', '.join(f'{t:.2f}' for t in times)} s)")
 
 
 def pmc_traffic(kernel: str):
@@ -85,6 +111,47 @@ def pmc_traffic(kernel: str):
     return None
 
 
+def extra_configs(pipe, a):
+    """BASELINE configs[3] (C4: B=64 prompts, 4 LCM steps, batch-doubled classifier-free guidance at scale 5) and
+    configs[4] (C5: B=16 latents of 30 s, VAE decode + BigVGAN only: the DiT caps at T <= 845) on one GPU,
+    timed like the headline (warm-up, synchronise, K steps), each with the §8(d) model roofline fraction."""
+    from audiolcm_amd import recipe, roofline as RL
+    out = {}
+    # C4
+    B, S, T = 64, 4, 312
+    ids = list(range(B))
+    cond = torch.cat([recipe.synthetic_context(1, seed0=1000 + i) for i in ids], 0).cuda()
+    uc = torch.cat([recipe.synthetic_context(1, seed0=900 + i) for i in ids], 0).cuda()
+
+    def c4():
+        pipe.generate(cond, seeds=ids, steps=S, latent_len=T, unconditional=uc, cfg_scale=5.0)
+    # C5
+    B5, T5 = 16, 936
+    z5 = torch.randn((B5, 20, T5), generator=torch.Generator().manual_seed(5)).cuda()
+
+    def c5():
+        pipe.decode(z5)
+    for name, fn, kw, audio in (("config4", c4, RL.CONFIGS[4], B * T * 2 * HOP / SR),
+                                ("config5", c5, RL.CONFIGS[5], B5 * T5 * 2 * HOP / SR)):
+        for _ in range(max(1, a.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        roof = RL.summary(RL.path_layers(**kw))
+        out[name] = dict(value=round(audio / dt, 2), unit="audio-s/s", ms_per_step=round(1e3 * dt, 2),
+                         path_roofline_frac_model=round(roof["t_roof_ms"] / (1e3 * dt), 4),
+                         t_roof_ms=round(roof["t_roof_ms"], 2), ideal_value=round(audio / roof["t_roof_ms"] * 1e3, 1),
+                         workload=("BASELINE configs[3]: 64 prompts, 4 LCM steps, batch-doubled CFG (scale 5, "
+                                   "128-row DiT calls), 9.984 s clips" if name == "config4" else
+                                   "BASELINE configs[4]: 16 latents of 20x936 -> mel 80x1872 -> 479,232 samples "
+                                   "(29.952 s), VAE decode + BigVGAN"))
+    return out
+
+
 def main():
     a = parse()
     from audiolcm_amd import _hip, recipe
@@ -92,6 +159,8 @@ def main():
     from audiolcm_amd.pipeline import AudioLCMPipeline
     import torch.distributed as dist
 
+    from audiolcm_amd import roofline as RL
+    model_roof = RL.summary(RL.path_layers(B=a.batch, S=a.lcm_steps, T=a.latent_len))
     rank, world, local = init_from_env()
     torch.cuda.set_device(local)
     _hip.require_device(local)
@@ -136,11 +205,9 @@ def main():
     value = world * B * clip_sec * a.steps / dt
     # roofline pass: the same steps with live HIP-event timing of every launch and the resblock streams
     # serialised, so a kernel's measured duration is its own (concurrent kernels would share the chip)
-    prev = os.environ.get("ALCM_SERIAL_RESBLOCKS")
-    os.environ["ALCM_SERIAL_RESBLOCKS"] = "1"
+    pipe.vocoder.set_resblock_streams(False)
     dt_prof, prof = timed(a.steps, True)
-    if prev is None:
-        os.environ.pop("ALCM_SERIAL_RESBLOCKS")
+    pipe.vocoder.set_resblock_streams(True)
     gpu_ms = sum(p["total_ms"] for p in prof)
     dom = max(prof, key=lambda p: p["total_ms"]) if prof else None
     roofline = None
@@ -156,8 +223,16 @@ def main():
                         avg_launch_us=round(1e3 * dom["total_ms"] / dom["launches"], 2),
                         per_launch_algorithmic=round((dom["flops"] if mfma else dom["bytes"]) / dom["launches"], 1),
                         kernel_share_of_gpu_time=round(dom["total_ms"] / max(gpu_ms, 1e-9), 4),
-                        path_roofline_frac=round(sum(p["roof_ms"] for p in prof) / (1e3 * dt), 4),
-                        path_roofline_note="sum over all kernel launches of max(F/2.5PF, B/8TB/s) / headline wall",
+                        path_roofline_frac_model=round(model_roof["t_roof_ms"] / (1e3 * dt / a.steps), 4),
+                        path_roofline_model=dict(
+                            t_roof_ms=round(model_roof["t_roof_ms"], 3), gflop=round(model_roof["gflop"], 1),
+                            gbytes=round(model_roof["gbytes"], 2),
+                            ideal_value=round(B * clip_sec / model_roof["t_roof_ms"] * 1e3, 1),
+                            note="SURVEY.md §8(d) model (audiolcm_amd/roofline.py): bf16 layer-boundary bytes, "
+                                 "sum over layers of max(F/2.5PF, B/8TB/s); frac = t_roof / ms_per_step"),
+                        path_roofline_frac_build=round(sum(p["roof_ms"] for p in prof) / (1e3 * dt), 4),
+                        path_roofline_note_build="sum over this build's kernel launches of max(F/2.5PF, B/8TB/s) "
+                                                 "(fp32 activations, unfused byte counts) / headline wall",
                         measured_in=f"separate timed pass of the same {a.steps} steps, per-launch HIP events on the "
                                     f"launch streams, resblock streams serialised ({1e3 * dt_prof / a.steps:.2f} "
                                     f"ms/step)")
@@ -175,6 +250,8 @@ def main():
                             global_batch=B * world, per_gpu_batch=B, lcm_steps=S, latent_len=T,
                             parallelism=f"dp{world} (prompt shards, RCCL all-gather of waveforms)"),
                 roofline=roofline)
+    if world == 1 and a.extra_configs:
+        line["other_configs"] = extra_configs(pipe, a)
     if world == 1 and a.also_other_mode:
         for other in ("mixed", "split", "bf16"):
             if other == a.mode:

@@ -89,7 +89,10 @@ def save(name, **arrays):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated fixture groups to (re)generate: base, c2, c4, c5 "
+                                               "(default: all)")
     args = ap.parse_args()
+    groups = set(filter(None, args.only.split(","))) or {"base", "c2", "c4", "c5"}
     install_stubs()
     sys.path.insert(0, args.ref)
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
@@ -137,9 +140,70 @@ def main():
     assert dit_keys == set(Sd.keys()), sorted(dit_keys ^ set(Sd.keys()))[:10]
 
     with torch.no_grad():
-        # ---- schedule / embeddings / step -------------------------------------------------
         smp = LCMSampler(lcm)
         smp.make_schedule(verbose=False)
+        orig = scheduling_lcm.torch.randn
+        if "base" in groups:
+            base_fixtures(lcm, smp, voc, scheduling_lcm, orig, meta, Activation1d, SnakeBeta)
+        if "c2" in groups:
+            # ---- config 2, last prompt of the bench batch: seed 31, context seed 1031 (bench.py ids 0..31) ----
+            xT, noise = recipe.prompt_noise([31], 2, 20, 312)
+            c = recipe.synthetic_context(1, seed0=1031)
+            calls = {"i": 0}
+
+            def fake_randn31(*a, **k):
+                calls["i"] += 1
+                return noise[calls["i"] - 1].clone()
+            scheduling_lcm.torch.randn = fake_randn31
+            try:
+                z, _ = smp.sample(S=2, conditioning=c, batch_size=1, shape=[20, 312], verbose=False,
+                                  guidance_scale=5, original_inference_steps=50, x_T=xT.clone())
+            finally:
+                scheduling_lcm.torch.randn = orig
+            mel = lcm.decode_first_stage(z)
+            save("e2e_S2_prompt31.npz", x_T=xT, noise=noise, latent=z, mel=mel, wav=voc(mel).squeeze(1))
+        if "c5" in groups:
+            # ---- config 5: 30-s long-form vocoder leg (M = 1872 mel frames -> 479,232 samples) ---------
+            gm = torch.Generator().manual_seed(300 + 1872)
+            mel = torch.randn((1, 80, 1872), generator=gm) * 1.5 - 4.0
+            save("bigvgan_M1872.npz", mel=mel, wav=voc(mel))
+        if "c4" in groups:
+            # ---- config 4: 4 LCM steps with batch-doubled classifier-free guidance at T = 312 ---------
+            # The reference LCMSampler has no CFG (scheduling_lcm.py:359-377); config 4 composes the reference
+            # pieces: the [uc; c] batch-doubled DiT call and combine of ddim.py:203-205 / plms.py:184-186, then
+            # the reference LCMSampler.step (scheduling_lcm.py:410-496) with the recorded step noise.
+            S, B, T, scale = 4, 2, 312, 5.0
+            xT, noise = recipe.prompt_noise([5, 6], S, 20, T)
+            c = recipe.synthetic_context(B)
+            uc = recipe.synthetic_context(B, seed0=900)
+            smp.set_timesteps(S, original_inference_steps=50)
+            smp._step_index = None
+            w = torch.tensor(5 - 1).repeat(2 * B)
+            wemb = smp.get_guidance_scale_embedding(w, embedding_dim=256)
+            img = xT.clone()
+            calls = {"i": 0}
+
+            def fake_randn(*a, **k):
+                i = calls["i"]
+                calls["i"] += 1
+                return noise[i].clone()
+            scheduling_lcm.torch.randn = fake_randn
+            try:
+                for t in smp.timesteps:
+                    ts = torch.full((2 * B,), int(t), dtype=torch.long)
+                    e = lcm.apply_model(torch.cat([img, img]), ts, torch.cat([uc, c]), lcm.unet, w_cond=wemb)
+                    e_u, e_c = e.chunk(2)
+                    img, den = smp.step(e_u + scale * (e_c - e_u), t, img, return_dict=False)
+            finally:
+                scheduling_lcm.torch.randn = orig
+            assert calls["i"] == S - 1
+            save("e2e_cfg_S4_B2_T312.npz", x_T=xT, noise=noise, context_seed0=1000, uncond_seed0=900, cfg_scale=scale, latent=den,
+                 mel=lcm.decode_first_stage(den))
+
+
+def base_fixtures(lcm, smp, voc, scheduling_lcm, orig, meta, Activation1d, SnakeBeta):
+    if True:
+        # ---- schedule / embeddings / step -------------------------------------------------
         sched = {}
         for S in (1, 2, 4, 8):
             smp.set_timesteps(S, original_inference_steps=50)
@@ -157,7 +221,6 @@ def main():
         smp.set_timesteps(2, original_inference_steps=50)
         smp.num_inference_steps = 2
         smp._step_index = None
-        orig = scheduling_lcm.torch.randn
         scheduling_lcm.torch.randn = lambda *a, **k: nz.clone()
         try:
             prev0, den0 = smp.step(eps, 999, x, return_dict=False)

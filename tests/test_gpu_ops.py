@@ -153,10 +153,12 @@ def test_flash_attention(K, B, L, heads, dh, prec):
 
 
 @pytest.mark.parametrize("prec", [2, 0])
-def test_feedforward_on_planes(K, prec):
+@pytest.mark.parametrize("L", [300, 700])
+def test_feedforward_on_planes(K, prec, L):
     """DiT Conv1dFeedForward on operand planes: LayerNorm -> plane, conv k9 with the GEGLU plane epilogue
-    (interleaved value/gate columns), conv k9 + residual — vs fp32 F.conv1d / F.gelu."""
-    B, L, H, inner, k = 2, 300, 576, 2304, 9
+    (interleaved value/gate columns), conv k9 + residual — vs fp32 F.conv1d / F.gelu.  L = 700 (1400 rows)
+    puts the 2304 -> 576 conv on the wide-layer kernel, as at the bench's B = 32 (alcm_wconv.hip)."""
+    B, H, inner, k = 2, 576, 2304, 9
     x = _r((B, L, H), 110)
     gam, bet = 1 + _r((H,), 111, 0.1), _r((H,), 112, 0.1)
     w0, b0 = _r((2 * inner, H, k), 113, 1 / np.sqrt(H * k)), _r((2 * inner,), 114, 0.05)
@@ -175,6 +177,37 @@ def test_feedforward_on_planes(K, prec):
     assert rel_l2(dec(p2[0].cpu()).numpy(), gg.permute(0, 2, 1).numpy()) < TOL[prec]
     y = K.opconv(p2, inner, dev(w2), dev(b2), 1, prec, residual=dev(x)).cpu()
     assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+
+
+@pytest.mark.parametrize("N,rows", [(1728, 600), (1728, 1400), (576, 600), (576, 1400), (576, 2 * 4 * 467)])
+@pytest.mark.parametrize("prec", [0, 2])
+def test_opconv_dit_projection_shapes(K, N, rows, prec):
+    """The DiT attention projections on operand planes: fused q/k/v (576 -> 1728, k = 1) and to_out (576 -> 576,
+    + bias + residual) at row counts below (opconv_kernel) and above (wide-layer kernel) the 1024-row switch,
+    up to the bench's B = 32 x 467 rows divided over several launches' worth (3736 rows)."""
+    B, H = 2, 576
+    L = rows // B
+    x = _r((B, L, H), 130)
+    w, bias = _r((N, H, 1), 131, 1 / np.sqrt(H)), _r((N,), 132, 0.05)
+    r = _r((B, L, N), 133)
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias).permute(0, 2, 1) + r
+    pl = K.operand_planes(dev(x), prec)
+    y = K.opconv(pl, H, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+
+
+def test_group_norm_stats_large_mean(K):
+    """One-pass (fp64 sum / sum of squares) GroupNorm statistics on data whose mean is 1e4 x its standard
+    deviation (the cancellation case of E[x^2] - mean^2): the normalised output matches F.group_norm."""
+    B, C, T = 2, 32, 3200   # 1e5 elements per (b, group) with 2 groups
+    xf = (_r((B, C, T), 140, 0.1).double() + 1e3).float()
+    g, b = 1 + _r((C,), 141, 0.1), _r((C,), 142, 0.1)
+    ref = F.group_norm(xf.double(), 2, g.double(), b.double(), 1e-6)
+    sc, sh = K.group_norm_affine(dev(xf.permute(0, 2, 1).contiguous()), 2, dev(g), dev(b), 1e-6)
+    y = xf.double() * sc.cpu().double()[:, :, None] + sh.cpu().double()[:, :, None]
+    # the fp32 scale (~10) and shift (~-1e4) carry ~1e-3 absolute rounding on y = x*scale + shift; an fp32
+    # one-pass variance would be off by ~0.06 against the true 0.01 (y wrong by O(1))
+    assert (y - ref).abs().max().item() < 3e-3
 
 
 def test_linear_and_layer_norm(K):

@@ -195,3 +195,19 @@ def test_api_requires_checkpoints(tmp_path):
     with pytest.raises(FileNotFoundError):
         AudioLCMBatchInfer(["x"], config_path=os.path.join(REPO, "configs", "audiolcm.yaml"),
                            model_path=str(tmp_path / "missing.ckpt"), outpath=str(tmp_path))
+
+
+def test_roofline_model_reproduces_survey():
+    """audiolcm_amd/roofline.py (bench.py's path_roofline_frac_model) reproduces SURVEY.md §8(d) / BASELINE.md §3:
+    C2 47,763 GFLOP / 20.9 ms, C4 ~153.4k GFLOP / 65.3 ms, C5 57,243 GFLOP / 25.45 ms."""
+    from audiolcm_amd import roofline as RL
+    c2 = RL.summary(RL.path_layers(**RL.CONFIGS[2]))
+    c4 = RL.summary(RL.path_layers(**RL.CONFIGS[4]))
+    c5 = RL.summary(RL.path_layers(**RL.CONFIGS[5]))
+    assert abs(c2["gflop"] - 47763) / 47763 < 1e-3 and abs(c2["t_roof_ms"] - 20.9) < 0.1
+    assert abs(c4["gflop"] - 153400) / 153400 < 5e-3 and abs(c4["t_roof_ms"] - 65.3) < 0.3
+    assert abs(c5["gflop"] - 57243) / 57243 < 1e-3 and abs(c5["t_roof_ms"] - 25.45) < 0.1
+    dit = RL.summary(RL.dit_layers(1, 312))
+    assert abs(dit["gflop"] - 150.6) < 0.5           # per sample-step (SURVEY §8a a9)
+    assert abs(RL.summary(RL.vae_layers(1, 312))["gflop"] - 65.8) < 0.2
+    assert abs(RL.summary(RL.bigvgan_layers(1, 624))["gflop"] - 1125.5) < 0.5

@@ -123,3 +123,27 @@ def test_pcm16_quantiser():
     b = O.pcm16_bytes(np.array([0.0, 1.0, -1.0, 0.5, 2.0], dtype=np.float32))
     v = np.frombuffer(b, dtype="<i2")
     assert list(v) == [0, 32767, -32767, 16384, 32767]
+
+
+def test_cfg_composition_config4(states):
+    """Config 4 (S=4, batch-doubled CFG, T=312, B=2): the oracle composition vs the reference pieces."""
+    g = golden("e2e_cfg_S4_B2_T312.npz")
+    ctx = recipe.synthetic_context(2, seed0=int(g["context_seed0"]))
+    uc = recipe.synthetic_context(2, seed0=int(g["uncond_seed0"]))
+    scale = float(g["cfg_scale"])
+
+    def eps_fn(x, t, w):
+        e = O.dit_forward(states["dit"], torch.cat([x, x]), torch.cat([t, t]), torch.cat([uc, ctx]),
+                          torch.cat([w, w]))
+        e_u, e_c = e.chunk(2)
+        return O.cfg_combine(e_u, e_c, scale)
+    z = O.lcm_sample(eps_fn, ctx, torch.from_numpy(g["x_T"]), torch.from_numpy(g["noise"]), 4)
+    assert rel_l2(z.numpy(), g["latent"]) < 1e-5
+
+
+def test_bigvgan_long_form_config5(states):
+    """Config 5 vocoder leg: 1872 mel frames (30 s) -> 479,232 samples."""
+    g = golden("bigvgan_M1872.npz")
+    wav = O.bigvgan_forward(states["bigvgan"], torch.from_numpy(g["mel"]))
+    assert wav.shape == g["wav"].shape
+    assert rel_l2(wav.numpy(), g["wav"]) < 1e-5
