@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
         bool st = mok && n < P.N;
         if (E.geglu) {
           const float g = __shfl_xor(v, 1);
-          v = v * alcm_act(g, ACT_GELU_ERF);
+          v = v * alcm_act(g, E.geglu == 2 ? ACT_GELU_TANH : ACT_GELU_ERF);
           st = st && ((lane & 1) == 0);
           nout = n >> 1;
         } else if (E.act) {
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const GemmDev P, int tiles_pe
         bool st = mok && n < P.N;
         if (E.geglu) {
           const float g = __shfl_xor(v, 1);
-          v = v * alcm_act(g, ACT_GELU_ERF);
+          v = v * alcm_act(g, E.geglu == 2 ? ACT_GELU_TANH : ACT_GELU_ERF);
           st = st && ((lane & 1) == 0);
           nout = n >> 1;
         } else if (E.act) {

@@ -61,7 +61,8 @@ int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const voi
 
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
-  int wconv = 5;                 // ALCM_WCONV: 0 = never the wide-layer kernel, 7 = setprio K loop
+  int wconv = 8;                 // ALCM_WCONV: 8 = 2-workgroup/CU kernel, 5 = 256-row kernel, 0 = neither
+  int wconv_ablate = 0;          // ALCM_WCONV_ABLATE: timing-only ablation bits of the wide-layer kernel
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width
   int nconv_nb = 0;              // ALCM_NCONV_NB: narrow-conv ring depth / tile variant
   int act_rows = 8;              // ALCM_ACT_ROWS: rows per thread of the per-thread Activation1d kernel

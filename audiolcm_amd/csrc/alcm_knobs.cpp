@@ -17,7 +17,8 @@ static bool env_set(const char* name) {
 
 static Knobs read_knobs() {
   Knobs k;
-  k.wconv = env_int("ALCM_WCONV", 5);
+  k.wconv = env_int("ALCM_WCONV", 8);
+  k.wconv_ablate = env_int("ALCM_WCONV_ABLATE", 0);
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;

@@ -46,6 +46,8 @@ struct WConvDev {
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
+  int ablate;           // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue,
+                        // 2 no MFMA, 4 no global -> LDS staging in the K loop
 };
 
 constexpr int WC_BM = 256;
@@ -101,11 +103,14 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
     const int ls = (lane & 7) ^ (n & 7);
     bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
   }
+  const bool no_dma = (P.ablate & 4) != 0, no_mfma = (P.ablate & 2) != 0;
   auto stage_w = [&](int c, int buf) {
+    if (no_dma && c > 0) return;
 #pragma unroll
     for (int j = 0; j < WC_WPW; ++j) glds16(wsrc[j] + c * wstep[j], smem + buf * WBUF + (wave + 8 * j) * 1024);
   };
   auto stage_b = [&](int s, int buf) {
+    if (no_dma && s > 1) return;
     const int c = s / K, tap = s - c * K;
     const int off = tap * Cp + c * 64;
 #pragma unroll
@@ -154,6 +159,13 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
           const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
 #pragma unroll
           for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
+          if (no_mfma) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bfr[j]));
+            continue;
+          }
 #pragma unroll
           for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -193,6 +205,15 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (P.ablate & 1) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    asm volatile("" ::"v"(sum));
+    return;
+  }
 
   if constexpr (ACT) {
     // v = conv + bias (+ res) -> LDS, one half of the tile's columns at a time (all 256 rows: the
@@ -337,6 +358,185 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Two-workgroups-per-CU variant (ALCM_WCONV=8): tile 128 rows x 192 columns, 4 waves as 2 (M) x 2 (N), each
+// wave 64 x 96 (4 x 6 16x16x32 MFMAs per 32-deep K slice, 0.42 fragment reads per MFMA).  72 KB of LDS
+// (one input window of <= 192 rows x 64 channels + two weight tiles) so two workgroups share a CU: the
+// HBM-bound epilogue (fp32 output + residual + accumulate) of one overlaps the MFMA K loop of the other,
+// where the 256-row kernel above serialises them (its epilogue is 26-80 % of its time on the BigVGAN shapes,
+// scripts/microbench.py wablate).  K steps: weights double-buffered (step s+1 staged while step s computes,
+// vmcnt(0) + barrier per step); the window is single-buffered and re-staged at each 64-channel chunk
+// boundary (the stall is covered by the other workgroup).
+constexpr int W2_BM = 128, W2_BN = 192, W2_WROWS = 192;
+
+template <int PREC, bool GEGLU>
+__global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
+  constexpr int TM = 4, TN = 6;
+  constexpr int WBUF = W2_WROWS * 128;   // window image (24 KB)
+  constexpr int BBUF = W2_BN * 128;      // weight image (24 KB)
+  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB
+  constexpr int WPW = W2_WROWS / 8 / 4;  // window DMA instructions per wave (6)
+  constexpr int BPW = W2_BN / 8 / 4;     // weight DMA instructions per wave per step (6)
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = P.nwg >> 3, r8 = P.nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int mt = wid / P.tiles_n, nt = wid - mt * P.tiles_n;
+  const int b = mt / P.tiles_per_batch;
+  const int t0 = (mt - b * P.tiles_per_batch) * W2_BM;
+  const int col0 = nt * W2_BN;
+  const int K = P.ksize, Cp = P.Cp;
+  const int WR = W2_BM + (K - 1) * P.dil;
+  const int nC = Cp / 64;
+  const int steps = nC * K;
+
+  const u16* wsrc[WPW];
+  int wstep[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int row = 8 * (wave + 4 * j) + (lane >> 3);
+    const int ls = (lane & 7) ^ (row & 7);
+    const int ts = t0 - P.pad + row;
+    const bool ok = row < WR && ts >= 0 && ts < P.T;
+    wsrc[j] = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
+    wstep[j] = ok ? 64 : 0;
+  }
+  const u16* bsrc[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int n = 8 * (wave + 4 * j) + (lane >> 3);
+    const int ls = (lane & 7) ^ (n & 7);
+    bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
+  }
+  auto stage_w = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + c * wstep[j], smem + (wave + 4 * j) * 1024);
+  };
+  auto stage_b = [&](int st, int buf) {
+    const int c = st / K, tap = st - c * K;
+    const int off = tap * Cp + c * 64;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) glds16(bsrc[j] + off, smem + WBUF + buf * BBUF + (wave + 4 * j) * 1024);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow0 = wm * 64 + (lane & 15);
+  const int nrow0 = wn * 96 + (lane & 15);
+  const int bsw = lane & 7;
+
+  stage_w(0);
+  stage_b(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  int st = 0;
+  for (int c = 0; c < nC; ++c) {
+    for (int tap = 0; tap < K; ++tap, ++st) {
+      if (st + 1 < steps) stage_b(st + 1, (st + 1) & 1);
+      const char* Bl = smem + WBUF + (st & 1) * BBUF;
+      const int arow = arow0 + tap * P.dil;
+      const int asw = arow & 7;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int ls = 4 * sub + (lane >> 4);
+        bf16x8 af[TM], bfr[TN];
+        const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
+        const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+      }
+      if (tap == K - 1 && c + 1 < nC) {
+        // every wave has finished reading window c: re-stage it with chunk c + 1
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        stage_w(c + 1);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+
+  // epilogue: one 64-row half of the tile at a time through LDS (the K loop's last barrier retired every
+  // fragment read and DMA), whole 768-B row segments with 16-B loads / stores
+  constexpr int OTS = W2_BN + 4;
+  float* ot = reinterpret_cast<float*>(smem);
+  constexpr int cq = W2_BN / 4;
+  constexpr int PER = 64 * cq / 256;  // float4 per thread per half (12)
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            ot[(i * 16 + (lane >> 4) * 4 + r) * OTS + wn * 96 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int r0 = t0 + h * 64;
+    if constexpr (GEGLU) {
+      const int No = P.N / 2;
+      for (int e = 0; e < PER; ++e) {
+        const int idx = tid + e * 256;
+        const int m = idx / cq, n = (idx - m * cq) * 4;
+        if (r0 + m >= P.T) continue;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        if (P.bias) {
+          const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
+          v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+        }
+        f32x2 y;
+        y.x = v.x * alcm_act(v.y, ACT_GELU_ERF);
+        y.y = v.z * alcm_act(v.w, ACT_GELU_ERF);
+        op_store2<PREC>(P.gplane + ((int64_t)b * P.T + r0 + m) * No + (col0 + n) / 2, 0, y);
+      }
+    } else {
+      // two passes of PER/2 loads: the other half's accumulators are still live in half 0
+      constexpr int PH = PER / 2;
+#pragma unroll
+      for (int e0 = 0; e0 < PER; e0 += PH) {
+      float4 rv[PH], pv[PH];
+#pragma unroll
+      for (int e = 0; e < PH; ++e) {
+        const int idx = tid + (e0 + e) * 256;
+        const int m = idx / cq, n = (idx - m * cq) * 4;
+        const int t = min(r0 + m, P.T - 1);
+        const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + n;
+        rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
+        pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int e = 0; e < PH; ++e) {
+        const int idx = tid + (e0 + e) * 256;
+        const int m = idx / cq, n = (idx - m * cq) * 4;
+        if (r0 + m >= P.T) continue;
+        const int64_t go = ((int64_t)b * P.T + r0 + m) * P.N + col0 + n;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        if (P.bias) {
+          const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
+          v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+        }
+        v.x = (v.x + rv[e].x) * P.out_scale + pv[e].x;
+        v.y = (v.y + rv[e].y) * P.out_scale + pv[e].y;
+        v.z = (v.z + rv[e].z) * P.out_scale + pv[e].z;
+        v.w = (v.w + rv[e].w) * P.out_scale + pv[e].w;
+        *reinterpret_cast<float4*>(P.out + go) = v;
+      }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Eligible: single-plane precisions, N a multiple of 128, Cp a multiple of 64, 2 <= k, (k-1)d <= 64,
 // no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
@@ -352,12 +552,45 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
+  if (var == 8 && !act && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
+    WConvDev P{};
+    P.a = (const u16*)a.a;
+    P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
+    P.w = wplane; P.kpad = a.kpad; P.N = a.N;
+    P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+    P.gplane = (u16*)a.geglu_plane;
+    P.tiles_per_batch = (a.T + W2_BM - 1) / W2_BM;
+    P.tiles_n = a.N / W2_BN;
+    const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
+    if (nwg2 >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
+    P.nwg = (int)nwg2;
+    void* tok = prof_start(s);
+    const dim3 grid((unsigned)nwg2), blk(256);
+    const bool gl = a.geglu_plane != nullptr;
+    if (a.prec == PREC_F16) {
+      if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true>), grid, blk, 0, s, P);
+      else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false>), grid, blk, 0, s, P);
+    } else {
+      if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true>), grid, blk, 0, s, P);
+      else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false>), grid, blk, 0, s, P);
+    }
+    if (tok) {
+      char name[96];
+      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s>", a.prec, gl ? "true" : "false");
+      if (knobs().prof_shapes)
+        std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp,
+                      a.N, a.ksize);
+      prof_stop(tok, s, name, flops, bytes);
+    }
+    return 1;
+  }
   WConvDev P{};
   P.a = (const u16*)a.a;
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   P.gplane = (u16*)a.geglu_plane;
+  P.ablate = knobs().wconv_ablate;
   // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 256 conv rows and emits 256 - 2 * HALO
   P.tstride = act ? WC_BM - 2 * ACT_EPI_HALO : WC_BM;
   P.tshift = act ? ACT_EPI_HALO : 0;

@@ -102,7 +102,8 @@ typedef struct alcm_gemm_args {
   int batch, zdiv;
   alcm_operand a, b;
   /* activation codes: 0 none, 1 SiLU, 2 GELU (erf), 3 GELU (tanh), 4 tanh
-   * epilogue: v = acc*acc_scale + bias[n]; v = act(v) (geglu: v_even * gelu_erf(v_odd) -> column n/2);
+   * epilogue: v = acc*acc_scale + bias[n]; v = act(v) (geglu 1: v_even * gelu_erf(v_odd) -> column n/2,
+ *           geglu 2: v_even * gelu_tanh(v_odd), T5's gated-gelu with (wi_1, wi_0) rows interleaved);
    *           v += res[...]; v *= out_scale; if accumulate v += out[...]; out[...] = v
    * output row m -> (b, t), stored at out + zoff + b*o_sb + (t*out_step + out_off)*o_st + n*o_sc */
   const float* bias;

@@ -121,6 +121,57 @@ def bench_wconv(B=32):
                 print(f"C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line) + f" | max|diff| {diff:.2e}", flush=True)
 
 
+WIDE_SHAPES = [  # (name, T, Cin, N, k, dil, geglu, residual, accumulate) at B = 32
+    ("s0 C768 k11", 2496, 768, 768, 11, 5, False, True, False), ("s0 C768 k3", 2496, 768, 768, 3, 1, False, True, True),
+    ("s1 C384 k11", 9984, 384, 384, 11, 5, False, True, False), ("s1 C384 k3", 9984, 384, 384, 3, 1, False, True, True),
+    ("s2 C192 k11", 19968, 192, 192, 11, 5, False, True, False), ("s2 C192 k3", 19968, 192, 192, 3, 1, False, True, True),
+    ("dit ff0", 467, 576, 4608, 9, 1, True, False, False), ("dit ff2", 467, 2304, 576, 9, 1, False, True, False),
+    ("dit qkv", 467, 576, 1728, 1, 1, False, False, False), ("dit out", 467, 576, 576, 1, 1, False, True, False),
+    ("vae k3", 312, 1536, 1536, 3, 1, False, True, False)]
+
+
+def bench_wablate(B=32):
+    """wide-layer kernel phase costs (ALCM_WCONV_ABLATE bits: 1 no epilogue, 2 no MFMA, 4 no K-loop staging;
+    timing only) on every shape the bench runs it on"""
+    sel = os.environ.get("WSHAPES")
+    for name, T, Cin, N, k, d, gl, res, acc in WIDE_SHAPES:
+        if sel and not any(x in name for x in sel.split(",")):
+            continue
+        x = torch.randn((B, T, Cin), device="cuda")
+        w = torch.randn((N, Cin, k), device="cuda") / (Cin * k) ** 0.5
+        b = torch.randn(N, device="cuda") * 0.05
+        r = torch.randn((B, T, N), device="cuda") if res else None
+        o = torch.zeros((B, T, N), device="cuda") if acc else None
+        pw = K.pack_conv_weight(w)
+        pl = K.operand_planes(x, 2)
+        tf = 2 * B * T * Cin * N * k / 1e12
+        line, outs = [], []
+        for wc in os.environ.get("WCONV_VARS", "5").split(","):
+            os.environ["ALCM_WCONV"] = wc
+            for ab in os.environ.get("ABLATE", "0,1,2,4,6,3").split(","):
+                os.environ["ALCM_WCONV_ABLATE"] = ab
+                _hip.reload_knobs()
+                if gl:
+                    fn = lambda: K.opconv(pl, Cin, w, b, d, 2, packed=pw, geglu=True)
+                else:
+                    fn = lambda: K.opconv(pl, Cin, w, b, d, 2, residual=r, packed=pw, accumulate_into=o)
+                ms = timeit(fn, reps=5)
+                if ab == "0":
+                    if o is not None:
+                        o.zero_()
+                    y = fn()
+                    yy = y if y is not None else o
+                    outs.append((yy.view(torch.float16) if yy.dtype == torch.int16 else yy).float().clone())
+                line.append(f"w{wc}ab{ab} {ms:7.3f}")
+        os.environ.pop("ALCM_WCONV_ABLATE")
+        os.environ.pop("ALCM_WCONV")
+        _hip.reload_knobs()
+        ms0 = float(line[0].split()[1])
+        diff = max([float((outs[0] - x).abs().max()) for x in outs[1:]] or [0.0])
+        print(f"{name:12s} {tf / ms0 * 1e3:7.1f} TF/s | " + " | ".join(line) + f" ms | max|diff| {diff:.2e}",
+              flush=True)
+
+
 def bench_ffn(B=32):
     """DiT Conv1dFeedForward convs (L = 467 tokens): fp32-operand conv_kernel (LayerNorm prologue path) vs the
     wide-layer kernel on operand planes (GEGLU plane epilogue / residual epilogue)"""
@@ -195,4 +246,4 @@ if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["op", "conv", "act"]
     for w in which:
-        {"op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
+        {"wablate": bench_wablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()

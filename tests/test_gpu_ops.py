@@ -318,16 +318,18 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
     y = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5, accumulate_into=acc).cpu() - 1
     assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
     from audiolcm_amd import _hip
-    monkeypatch.setenv("ALCM_WCONV", "0")
-    _hip.reload_knobs()
-    try:
-        acc0 = dev(torch.ones((B, T, C)))
-        y0 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
-                      accumulate_into=acc0).cpu() - 1
-    finally:
-        monkeypatch.delenv("ALCM_WCONV")
+    # the default (2-workgroup/CU, 128 x 192 tiles) vs the 256-row kernel (ALCM_WCONV=5) and opconv_kernel (0)
+    for var in ("5", "0"):
+        monkeypatch.setenv("ALCM_WCONV", var)
         _hip.reload_knobs()
-    assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
+        try:
+            acc0 = dev(torch.ones((B, T, C)))
+            y0 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
+                          accumulate_into=acc0).cpu() - 1
+        finally:
+            monkeypatch.delenv("ALCM_WCONV")
+            _hip.reload_knobs()
+        assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
 
 
 @pytest.mark.parametrize("C,T,k,dil,prec", [(24, 1000, 11, 5, 3), (48, 700, 7, 3, 3), (96, 500, 3, 1, 3),
