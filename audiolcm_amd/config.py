@@ -21,7 +21,7 @@ TARGET_ALIASES: Dict[str, str] = {
     "ldm.models.autoencoder1d.AutoencoderKL": "audiolcm_amd.models.AutoencoderKL",
     "vocoder.bigvgan.models.VocoderBigVGAN": "audiolcm_amd.models.VocoderBigVGAN",
     "vocoder.bigvgan.models.BigVGAN": "audiolcm_amd.models.BigVGAN",
-    "ldm.modules.encoders.modules.FrozenCLAPFLANEmbedder": "audiolcm_amd.conditioning.FrozenCLAPFLANEmbedder",
+    "ldm.modules.encoders.modules.FrozenCLAPFLANEmbedder": "audiolcm_amd.text_encoder.FrozenCLAPFLANEmbedder",
     "ldm.models.diffusion.scheduling_lcm.LCMSampler": "audiolcm_amd.lcm.LCMSampler",
 }
 # accepted but inert at inference (training-only components named by the YAML)

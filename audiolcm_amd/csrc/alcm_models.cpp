@@ -28,6 +28,14 @@ int set_error(int code, const std::string& msg) {
 
 int sincos_embedding(const float* v, float vscale, const float* freqs, int B, int half, int cos_first, float* out,
                      hipStream_t s);
+// alcm_text.hip
+int embed_gather(const int64_t* ids, int rows, const float* table, int64_t vocab, int D, const float* add, int L,
+                 float* out, hipStream_t s);
+int rms_stats(const float* x, int rows, int C, float eps, float* mean, float* rstd, hipStream_t s);
+int rms_norm(const float* x, int rows, int C, float eps, const float* w, int L, int64_t out_sb, float* out,
+             hipStream_t s);
+int softmax_rows_bias(float* x, int rows, int n, int64_t ld, int L, int heads, const float* bias, int bld,
+                      hipStream_t s);
 int i64_to_f32(const int64_t* t, float* o, int n, hipStream_t s);
 
 // ------------------------------------------------------------------ weights
@@ -100,6 +108,35 @@ struct VocW {
   ActW post_act;
 };
 
+// text conditioning (FrozenCLAPFLANEmbedder, ldm/modules/encoders/modules.py:529-582)
+struct BertLayerW {  // transformers BertLayer (post-LN)
+  ConvW qkv, ao, inter, out;
+  NormW ln1, ln2;
+};
+struct T5BlockW {  // transformers T5Block of the encoder (pre-RMSNorm, no biases)
+  float* ln0 = nullptr;
+  float* ln1 = nullptr;
+  ConvW qkv, o, wi, wo;
+};
+struct TextW {
+  int b_vocab = 30522, b_hidden = 768, b_layers = 12, b_heads = 12, b_inter = 3072, b_maxpos = 512;
+  int p_out = 1024;
+  int t_vocab = 32128, t_d = 1024, t_dkv = 64, t_heads = 16, t_ff = 2816, t_layers = 24;
+  int max_len = 77;
+  float b_eps = 1e-12f, p_eps = 1e-5f, t_eps = 1e-6f;
+  float* b_word = nullptr;      // (vocab, hidden)
+  float* b_pos_type = nullptr;  // position_embeddings[t] + token_type_embeddings[0]  (maxpos, hidden)
+  NormW b_emb_ln;
+  std::vector<BertLayerW> bl;
+  ConvW p1, p2;  // CLAP Projection linear1 / linear2 (no bias)
+  NormW p_ln;
+  float* t_emb = nullptr;   // shared (vocab, d)
+  float* t_bias = nullptr;  // relative position bias (heads, max_len, max_len)
+  std::vector<T5BlockW> tb;
+  float* t_fin = nullptr;
+  float* zeros = nullptr;  // max(d, hidden) zeros: the RMSNorm prologue's shift
+};
+
 }  // namespace alcm
 
 struct alcm_model {
@@ -110,6 +147,7 @@ struct alcm_model {
   alcm::DitW dit;
   alcm::VaeW vae;
   alcm::VocW voc;
+  alcm::TextW text;
   // BigVGAN: the three resblocks of a stage are independent chains until their mean; they run on the
   // caller's stream plus two auxiliary streams ordered by events, so the VALU / HBM bound Activation1d
   // kernels of one chain overlap the MFMA-bound convs of another.  The auxiliary streams and events belong
@@ -1158,6 +1196,239 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   return plane_conv(s, G.post, w, B, T, 1, nullptr, wav, 1.f, 0, ACT_TANH, ppost);
 }
 
+// ------------------------------------------------------------------ text conditioning
+// FrozenCLAPFLANEmbedder.encode (ldm/modules/encoders/modules.py:567-582) from token ids:
+//   z  = Projection(BertModel(clap_ids).last_hidden_state)     CLAP/clap.py:8-20, transformers BertModel
+//   z2 = T5EncoderModel(t5_ids).last_hidden_state              transformers T5 (v1.1: gated-gelu, RMSNorm)
+//   out = concat([z, z2], dim=1)  -> (B, 2L, 1024)
+// Both encoders run without an attention mask (the reference passes input_ids only), so padding tokens attend.
+// Weight names are the embedder's state_dict keys: caption_encoder.base.* (BERT), caption_encoder.projection.*,
+// t5_transformer.* (Appendix A: cond_stage_model.* of the Lightning checkpoint, prefix stripped).
+static void build_text(Ingest& I, const int* ic, int nic) {
+  TextW& X = I.m->text;
+  if (nic >= 14) {
+    X.b_vocab = ic[0]; X.b_hidden = ic[1]; X.b_layers = ic[2]; X.b_heads = ic[3]; X.b_inter = ic[4];
+    X.b_maxpos = ic[5]; X.p_out = ic[6]; X.t_vocab = ic[7]; X.t_d = ic[8]; X.t_dkv = ic[9]; X.t_heads = ic[10];
+    X.t_ff = ic[11]; X.t_layers = ic[12]; X.max_len = ic[13];
+  }
+  const int H = X.b_hidden, D = X.t_d, TI = X.t_heads * X.t_dkv;
+  if (H % X.b_heads || (H / X.b_heads) % 8 || H % 4 || D % 4 || X.t_dkv % 8 || X.max_len > X.b_maxpos ||
+      X.max_len <= 0 || X.p_out % 4)
+    throw Error(ALCM_E_INVALID, "unsupported text-encoder geometry");
+  const std::string bp = "caption_encoder.base.", pp = "caption_encoder.projection.", tp = "t5_transformer.";
+  // BERT embeddings: word + position + token_type[0] (token_type_ids default to zeros), then LayerNorm
+  X.b_word = I.upload(I.get(bp + "embeddings.word_embeddings.weight", {X.b_vocab, H}));
+  {
+    std::vector<float> pos = I.get(bp + "embeddings.position_embeddings.weight", {X.b_maxpos, H});
+    const int64_t ntt = I.has(bp + "embeddings.token_type_embeddings.weight") ?
+        I.by.at(bp + "embeddings.token_type_embeddings.weight")->shape[0] : 0;
+    if (ntt <= 0) throw Error(ALCM_E_MISSING, "missing weight tensor '" + bp + "embeddings.token_type_embeddings.weight'");
+    std::vector<float> tt = I.get(bp + "embeddings.token_type_embeddings.weight", {ntt, H});
+    for (int t = 0; t < X.b_maxpos; ++t)
+      for (int c = 0; c < H; ++c) pos[(size_t)t * H + c] += tt[c];
+    X.b_pos_type = I.upload(pos);
+  }
+  X.b_emb_ln = I.norm(bp + "embeddings.LayerNorm.", H);
+  for (int l = 0; l < X.b_layers; ++l) {
+    const std::string p = bp + "encoder.layer." + std::to_string(l) + ".";
+    BertLayerW L;
+    std::vector<float> w, b;
+    for (const char* q : {"query", "key", "value"}) {
+      auto wq = I.get(p + "attention.self." + q + ".weight", {H, H});
+      auto bq = I.get(p + "attention.self." + q + ".bias", {H});
+      w.insert(w.end(), wq.begin(), wq.end());
+      b.insert(b.end(), bq.begin(), bq.end());
+    }
+    L.qkv.w = I.pack(w, 3 * H, H, 1);
+    L.qkv.b = I.upload(b);
+    L.ao = I.linear(p + "attention.output.dense.", H, H);
+    L.ln1 = I.norm(p + "attention.output.LayerNorm.", H);
+    L.inter = I.linear(p + "intermediate.dense.", X.b_inter, H);
+    L.out = I.linear(p + "output.dense.", H, X.b_inter);
+    L.ln2 = I.norm(p + "output.LayerNorm.", H);
+    X.bl.push_back(L);
+  }
+  X.p1 = I.linear(pp + "linear1.", X.p_out, H, false);
+  X.p2 = I.linear(pp + "linear2.", X.p_out, X.p_out, false);
+  X.p_ln = I.norm(pp + "layer_norm.", X.p_out);
+  // T5 encoder
+  const std::string emb = I.has(tp + "shared.weight") ? tp + "shared.weight" : tp + "encoder.embed_tokens.weight";
+  X.t_emb = I.upload(I.get(emb, {X.t_vocab, D}));
+  {
+    // relative position bias of block 0 (shared by every block): bias[h][i][j] = table[bucket(j - i)][h]; the
+    // bucket table (T5Attention._relative_position_bucket, bidirectional) comes from the host as a tensor
+    const int ML = X.max_len;
+    auto bk = I.get("_alcm.t5_rel_buckets", {ML, ML});
+    const std::string rb = tp + "encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight";
+    const int64_t nb = I.has(rb) ? I.by.at(rb)->shape[0] : 0;
+    if (nb <= 0) throw Error(ALCM_E_MISSING, "missing weight tensor '" + rb + "'");
+    auto tab = I.get(rb, {nb, X.t_heads});
+    std::vector<float> bias((size_t)X.t_heads * ML * ML);
+    for (int h = 0; h < X.t_heads; ++h)
+      for (int i = 0; i < ML; ++i)
+        for (int j = 0; j < ML; ++j) {
+          const int64_t k = (int64_t)bk[(size_t)i * ML + j];
+          if (k < 0 || k >= nb) throw Error(ALCM_E_INVALID, "relative position bucket out of range");
+          bias[((size_t)h * ML + i) * ML + j] = tab[(size_t)k * X.t_heads + h];
+        }
+    X.t_bias = I.upload(bias);
+  }
+  for (int l = 0; l < X.t_layers; ++l) {
+    const std::string p = tp + "encoder.block." + std::to_string(l) + ".layer.";
+    T5BlockW Bk;
+    Bk.ln0 = I.upload(I.get(p + "0.layer_norm.weight", {D}));
+    std::vector<float> w;
+    for (const char* q : {"q", "k", "v"}) {
+      auto wq = I.get(p + "0.SelfAttention." + q + ".weight", {TI, D});
+      w.insert(w.end(), wq.begin(), wq.end());
+    }
+    Bk.qkv.w = I.pack(w, 3 * TI, D, 1);
+    Bk.o = I.linear(p + "0.SelfAttention.o.", D, TI, false);
+    Bk.ln1 = I.upload(I.get(p + "1.layer_norm.weight", {D}));
+    // gated-gelu: rows interleaved (wi_1 j, wi_0 j) so the GEMM epilogue pairs value n and gate n^1
+    auto w0 = I.get(p + "1.DenseReluDense.wi_0.weight", {X.t_ff, D});
+    auto w1 = I.get(p + "1.DenseReluDense.wi_1.weight", {X.t_ff, D});
+    std::vector<float> wi((size_t)2 * X.t_ff * D);
+    for (int j = 0; j < X.t_ff; ++j) {
+      std::memcpy(&wi[(size_t)(2 * j) * D], &w1[(size_t)j * D], (size_t)D * sizeof(float));
+      std::memcpy(&wi[(size_t)(2 * j + 1) * D], &w0[(size_t)j * D], (size_t)D * sizeof(float));
+    }
+    Bk.wi.w = I.pack(wi, 2 * X.t_ff, D, 1);
+    Bk.wo = I.linear(p + "1.DenseReluDense.wo.", D, X.t_ff, false);
+    X.tb.push_back(Bk);
+  }
+  X.t_fin = I.upload(I.get(tp + "encoder.final_layer_norm.weight", {D}));
+  X.zeros = I.upload(std::vector<float>((size_t)std::max(D, H), 0.f));
+}
+
+struct TextWs {
+  float *x, *tmp, *qkv, *S, *O, *inter, *e1, *g, *mean, *rstd;
+};
+static TextWs plan_text(const TextW& X, Bump& bp, int B, int L) {
+  const size_t R = (size_t)B * L;
+  const int Lp = round_up(L, 8);
+  const size_t dmax = (size_t)std::max({X.b_hidden, X.t_d, X.p_out});
+  const size_t inner = (size_t)std::max(X.b_hidden, X.t_heads * X.t_dkv);
+  TextWs w;
+  w.x = bp.take<float>(R * dmax);
+  w.tmp = bp.take<float>(R * dmax);
+  w.qkv = bp.take<float>(R * 3 * inner);
+  w.S = bp.take<float>((size_t)B * std::max(X.b_heads, X.t_heads) * L * Lp);
+  w.O = bp.take<float>(R * inner);
+  w.inter = bp.take<float>(R * (size_t)std::max(X.b_inter, X.t_ff));
+  w.e1 = bp.take<float>(R * X.p_out);
+  w.g = bp.take<float>(R * X.p_out);
+  w.mean = bp.take<float>(R);
+  w.rstd = bp.take<float>(R);
+  return w;
+}
+
+// multi-head self-attention core on a fused qkv buffer (B, L, 3I), I = nh * dh:
+// O[b, t, h*dh + d] = softmax_j(scale * q_t . k_j (+ bias[h][t][j])) v_j  (no mask)
+static int mha(hipStream_t s, int prec, int B, int L, int nh, int dh, const float* qkv, float scale,
+               const float* bias, int bld, float* S, float* O) {
+  const int I = nh * dh, Lp = round_up(L, 8);
+  alcm_gemm_args g;
+  std::memset(&g, 0, sizeof(g));
+  g.M = L; g.N = L; g.Kpad = round_up(dh, kBK); g.batch = B * nh; g.zdiv = nh;
+  g.a.kind = ALCM_OPND_ACT; g.a.ptr = qkv; g.a.sb = 0; g.a.st = 3 * I; g.a.sc = 1;
+  g.a.T_in = L; g.a.C_in = dh; g.a.Cpad = dh; g.a.ksize = 1; g.a.dil = 1; g.a.up = 1; g.a.rows_per_batch = L;
+  g.a.zs1 = (int64_t)L * 3 * I; g.a.zs2 = dh;
+  g.b = g.a;
+  g.b.ptr = qkv + I;
+  g.acc_scale = scale;
+  g.out_scale = 1.f;
+  g.out = S; g.o_sb = 0; g.o_st = Lp; g.o_sc = 1; g.o_zs1 = (int64_t)nh * L * Lp; g.o_zs2 = (int64_t)L * Lp;
+  g.out_rows_per_batch = L; g.out_step = 1;
+  g.prec = prec;
+  ALCM_TRY(gemm(g, s));
+  if (bias) ALCM_TRY(softmax_rows_bias(S, B * nh * L, L, Lp, L, nh, bias, bld, s));
+  else ALCM_TRY(softmax_rows(S, B * nh * L, L, Lp, s));
+  alcm_gemm_args p;
+  std::memset(&p, 0, sizeof(p));
+  p.M = L; p.N = dh; p.Kpad = round_up(Lp, kBK); p.batch = B * nh; p.zdiv = nh;
+  p.a.kind = ALCM_OPND_ACT; p.a.ptr = S; p.a.sb = 0; p.a.st = Lp; p.a.sc = 1; p.a.T_in = L; p.a.C_in = Lp;
+  p.a.Cpad = Lp; p.a.ksize = 1; p.a.dil = 1; p.a.up = 1; p.a.rows_per_batch = L;
+  p.a.zs1 = (int64_t)nh * L * Lp; p.a.zs2 = (int64_t)L * Lp;
+  p.b.kind = ALCM_OPND_ACT_T; p.b.ptr = qkv + 2 * I; p.b.st = 3 * I; p.b.sc = 1; p.b.T_in = L; p.b.rows = dh;
+  p.b.zs1 = (int64_t)L * 3 * I; p.b.zs2 = dh;
+  p.acc_scale = 1.f; p.out_scale = 1.f;
+  p.out = O; p.o_sb = 0; p.o_st = I; p.o_sc = 1; p.o_zs1 = (int64_t)L * I; p.o_zs2 = dh;
+  p.out_rows_per_batch = L; p.out_step = 1;
+  p.prec = prec;
+  return gemm(p, s);
+}
+
+// y (R, N) = x (R, C) W^T (+ bias) with the conv helper (k = 1): rows are one "batch" of R tokens
+static int lin(hipStream_t s, int prec, int R, const float* x, int C, const ConvW& w, float* y, const ConvOpts& o) {
+  return conv(s, prec, 1, R, View{x, 0, C, 1, R, C}, w, Out{y, 0, w.w.rows, 1, 1, 0}, o);
+}
+
+static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5_ids, float* out, int B, int L,
+                       void* ws, size_t wsb, hipStream_t s) {
+  const TextW& X = m->text;
+  if (B <= 0 || L <= 0 || L > X.max_len) return set_error(ALCM_E_INVALID, "text_encode: L must be in [1, max_len]");
+  Bump bp(ws, wsb);
+  TextWs w = plan_text(X, bp, B, L);
+  if (!ws || bp.off > wsb) return set_error(ALCM_E_WORKSPACE, "text_encode: workspace too small");
+  const int R = B * L, H = X.b_hidden, D = X.t_d, TI = X.t_heads * X.t_dkv;
+  const int ps = prec_of(m, false);  // embeddings / norms / projection head: bf16x3 under every non-bf16 policy
+  const int pl = prec_of(m, true);   // the encoders' linears and attention (fp16 under the mixed policy)
+  // ---- CLAP text branch: BERT (post-LN), transformers BertModel with input_ids only
+  ALCM_TRY(embed_gather(clap_ids, R, X.b_word, X.b_vocab, H, X.b_pos_type, L, w.x, s));
+  ALCM_TRY(layer_norm(w.x, R, H, H, X.b_eps, X.b_emb_ln.g, X.b_emb_ln.b, nullptr, 0, w.x, H, s));
+  const int bdh = H / X.b_heads;
+  for (const BertLayerW& Ly : X.bl) {
+    ALCM_TRY(lin(s, pl, R, w.x, H, Ly.qkv, w.qkv, ConvOpts{}));
+    ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
+    ConvOpts ra;
+    ra.res = Res{w.x, 0, H, 1};
+    ALCM_TRY(lin(s, pl, R, w.O, H, Ly.ao, w.tmp, ra));
+    ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, nullptr, 0, w.x, H, s));
+    ConvOpts gi;
+    gi.act = ACT_GELU_ERF;
+    ALCM_TRY(lin(s, pl, R, w.x, H, Ly.inter, w.inter, gi));
+    ConvOpts ro;
+    ro.res = Res{w.x, 0, H, 1};
+    ALCM_TRY(lin(s, pl, R, w.inter, X.b_inter, Ly.out, w.tmp, ro));
+    ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln2.g, Ly.ln2.b, nullptr, 0, w.x, H, s));
+  }
+  // Projection: LayerNorm(e1 + linear2(gelu(e1))), e1 = linear1(h)  (dropout is the identity in eval)
+  ALCM_TRY(lin(s, ps, R, w.x, H, X.p1, w.e1, ConvOpts{}));
+  {
+    ConvOpts ga;
+    ga.act = ACT_GELU_ERF;
+    ALCM_TRY(lin(s, ps, R, w.x, H, X.p1, w.g, ga));
+    ConvOpts r2;
+    r2.res = Res{w.e1, 0, X.p_out, 1};
+    ALCM_TRY(lin(s, ps, R, w.g, X.p_out, X.p2, w.tmp, r2));
+    ALCM_TRY(layer_norm(w.tmp, R, X.p_out, X.p_out, X.p_eps, X.p_ln.g, X.p_ln.b, nullptr, 0, w.e1, X.p_out, s));
+    ALCM_HIP(hipMemcpy2DAsync(out, (size_t)2 * L * X.p_out * sizeof(float), w.e1, (size_t)L * X.p_out * sizeof(float),
+                              (size_t)L * X.p_out * sizeof(float), B, hipMemcpyDeviceToDevice, s));
+  }
+  // ---- T5 encoder (v1.1): pre-RMSNorm blocks, unscaled attention + relative position bias, gated-gelu FFN
+  ALCM_TRY(embed_gather(t5_ids, R, X.t_emb, X.t_vocab, D, nullptr, L, w.x, s));
+  for (const T5BlockW& Bk : X.tb) {
+    ALCM_TRY(rms_stats(w.x, R, D, X.t_eps, w.mean, w.rstd, s));
+    ConvOpts oq;
+    oq.pro = Pro{Bk.ln0, X.zeros, 0, w.mean, w.rstd, 0};
+    ALCM_TRY(lin(s, pl, R, w.x, D, Bk.qkv, w.qkv, oq));
+    ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
+    ConvOpts ro;
+    ro.res = Res{w.x, 0, D, 1};
+    ALCM_TRY(lin(s, pl, R, w.O, TI, Bk.o, w.x, ro));
+    ALCM_TRY(rms_stats(w.x, R, D, X.t_eps, w.mean, w.rstd, s));
+    ConvOpts of;
+    of.pro = Pro{Bk.ln1, X.zeros, 0, w.mean, w.rstd, 0};
+    of.geglu = 2;
+    ALCM_TRY(conv(s, pl, 1, R, View{w.x, 0, D, 1, R, D}, Bk.wi, Out{w.inter, 0, X.t_ff, 1, 1, 0}, of));
+    ConvOpts r2;
+    r2.res = Res{w.x, 0, D, 1};
+    ALCM_TRY(lin(s, pl, R, w.inter, X.t_ff, Bk.wo, w.x, r2));
+  }
+  return rms_norm(w.x, R, D, X.t_eps, X.t_fin, L, (int64_t)2 * L * D, out + (int64_t)L * D, s);
+}
+
 }  // namespace alcm
 
 // ------------------------------------------------------------------ C-ABI
@@ -1191,6 +1462,7 @@ extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, co
     if (kind == ALCM_MODEL_DIT) build_dit(I, iconfig, n_iconfig);
     else if (kind == ALCM_MODEL_VAE) build_vae(I, iconfig, n_iconfig);
     else if (kind == ALCM_MODEL_BIGVGAN) build_voc(I, iconfig, n_iconfig);
+    else if (kind == ALCM_MODEL_TEXT) build_text(I, iconfig, n_iconfig);
     else throw Error(ALCM_E_INVALID, "unknown model kind");
     if (hipDeviceSynchronize() != hipSuccess) throw Error(ALCM_E_HIP, "device sync after weight upload failed");
   } catch (const Error& e) {
@@ -1284,4 +1556,19 @@ extern "C" int alcm_bigvgan_forward(alcm_model* m, const float* mel, float* wav_
                                     size_t ws_bytes, alcm_stream_t stream) {
   if (!m || m->kind != ALCM_MODEL_BIGVGAN || !mel || !wav_out) return set_error(ALCM_E_INVALID, "bigvgan: bad args");
   return bigvgan_forward(m, mel, wav_out, B, M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t alcm_text_workspace_bytes(const alcm_model* m, int B, int L) {
+  if (!m || m->kind != ALCM_MODEL_TEXT) return 0;
+  Bump bp(nullptr, 0);
+  plan_text(m->text, bp, B, L);
+  return bp.off + 256;
+}
+
+extern "C" int alcm_text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5_ids, float* out, int B,
+                                int L, void* ws, size_t ws_bytes, alcm_stream_t stream) {
+  if (!m || m->kind != ALCM_MODEL_TEXT || !clap_ids || !t5_ids || !out)
+    return set_error(ALCM_E_INVALID, "text_encode: bad args");
+  if (m->text.p_out != m->text.t_d) return set_error(ALCM_E_INVALID, "text_encode: projection and T5 widths differ");
+  return text_encode(m, clap_ids, t5_ids, out, B, L, ws, ws_bytes, (hipStream_t)stream);
 }

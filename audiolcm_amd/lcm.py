@@ -56,7 +56,8 @@ class LCM_audio:
         self.model = self.unet  # `model`, `unet`, `target_unet` share weights at inference (lcm_audio.py:98-114)
         self.first_stage_model = (instantiate_from_config(first_stage_config, split=split) if first_stage_config
                                   else AutoencoderKL(split=split))
-        self.cond_stage_model = instantiate_from_config(cond_stage_config) if cond_stage_config else None
+        self.cond_stage_model = (instantiate_from_config(cond_stage_config, split=split) if cond_stage_config
+                                 else None)
 
     # -- weights ---------------------------------------------------------------------------------
     def load_state_dict(self, sd, strict=False):
@@ -70,6 +71,9 @@ class LCM_audio:
         fs = sub("first_stage_model.")
         if fs:
             self.first_stage_model.load_state_dict(fs)
+        cs = sub("cond_stage_model.")
+        if cs and self.cond_stage_model is not None and hasattr(self.cond_stage_model, "load_state_dict"):
+            self.cond_stage_model.load_state_dict(cs)
         if "scale_factor" in sd:
             self.scale_factor = float(sd["scale_factor"])
         return self
@@ -77,6 +81,8 @@ class LCM_audio:
     def load_recipe(self, seed: int = 0):
         self.unet.diffusion_model.load_state_dict(recipe.dit_state(seed))
         self.first_stage_model.load_state_dict(recipe.vae_state(seed))
+        if self.cond_stage_model is not None and hasattr(self.cond_stage_model, "load_state_dict"):
+            self.cond_stage_model.load_state_dict(recipe.text_state(seed))
         return self
 
     @property

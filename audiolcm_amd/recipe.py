@@ -317,6 +317,82 @@ def bigvgan_state(seed: int = 0, cfg: BigVGANConfig = BigVGANConfig()) -> Dict[s
     return make_state(bigvgan_specs(cfg), seed + 2)
 
 
+@dataclass(frozen=True)
+class TextConfig:
+    """FrozenCLAPFLANEmbedder (ldm/modules/encoders/modules.py:529-582): CLAP text tower = bert-base-uncased
+    (CLAP/config.yaml: transformer_embed_dim 768) + Projection(768 -> d_proj 1024) (CLAP/clap.py:8-20), and
+    the t5-v1_1-large encoder (d_model 1024, 16 heads x 64, d_ff 2816 gated-gelu, 24 blocks, 32 relative
+    buckets / max distance 128, RMSNorm eps 1e-6); max_length 77 tokens each."""
+    b_vocab: int = 30522
+    b_hidden: int = 768
+    b_layers: int = 12
+    b_heads: int = 12
+    b_inter: int = 3072
+    b_maxpos: int = 512
+    p_out: int = 1024
+    t_vocab: int = 32128
+    t_d: int = 1024
+    t_dkv: int = 64
+    t_heads: int = 16
+    t_ff: int = 2816
+    t_layers: int = 24
+    t_buckets: int = 32
+    t_max_distance: int = 128
+    max_len: int = 77
+
+    def iconfig(self) -> List[int]:
+        return [self.b_vocab, self.b_hidden, self.b_layers, self.b_heads, self.b_inter, self.b_maxpos, self.p_out,
+                self.t_vocab, self.t_d, self.t_dkv, self.t_heads, self.t_ff, self.t_layers, self.max_len]
+
+
+def text_specs(cfg: TextConfig = TextConfig()) -> List[Spec]:
+    """Keys of FrozenCLAPFLANEmbedder's state_dict on the inference path: ``caption_encoder.base.*``
+    (transformers BertModel), ``caption_encoder.projection.*`` (CLAP Projection) and ``t5_transformer.*``
+    (transformers T5EncoderModel; ``encoder.embed_tokens`` is tied to ``shared``).  Scales keep every
+    layer's activations O(1): T5 has no 1/sqrt(d) on its attention logits, so its q projection carries it."""
+    s: List[Spec] = []
+    H, bp = cfg.b_hidden, "caption_encoder.base."
+    s += [(bp + "embeddings.word_embeddings.weight", (cfg.b_vocab, H), "normal", 0.5),
+          (bp + "embeddings.position_embeddings.weight", (cfg.b_maxpos, H), "normal", 0.5),
+          (bp + "embeddings.token_type_embeddings.weight", (2, H), "normal", 0.5)]
+    s += _norm(bp + "embeddings.LayerNorm.", H)
+    for l in range(cfg.b_layers):
+        p = f"{bp}encoder.layer.{l}."
+        for q in ("query", "key", "value"):
+            s += _linear(f"{p}attention.self.{q}.", H, H)
+        s += _linear(p + "attention.output.dense.", H, H, gain=0.5)
+        s += _norm(p + "attention.output.LayerNorm.", H)
+        s += _linear(p + "intermediate.dense.", cfg.b_inter, H)
+        s += _linear(p + "output.dense.", H, cfg.b_inter, gain=0.5)
+        s += _norm(p + "output.LayerNorm.", H)
+    s += _linear(bp + "pooler.dense.", H, H)  # in the state_dict, unused by encode()
+    pp = "caption_encoder.projection."
+    s += _linear(pp + "linear1.", cfg.p_out, H, bias=False)
+    s += _linear(pp + "linear2.", cfg.p_out, cfg.p_out, bias=False, gain=0.5)
+    s += _norm(pp + "layer_norm.", cfg.p_out)
+    D, I, tp = cfg.t_d, cfg.t_heads * cfg.t_dkv, "t5_transformer."
+    s += [(tp + "shared.weight", (cfg.t_vocab, D), "normal", 1.0)]
+    for l in range(cfg.t_layers):
+        p = f"{tp}encoder.block.{l}.layer."
+        s += [(p + "0.SelfAttention.q.weight", (I, D), "fanin", cfg.t_dkv ** -0.5),
+              (p + "0.SelfAttention.k.weight", (I, D), "fanin", 1.0),
+              (p + "0.SelfAttention.v.weight", (I, D), "fanin", 1.0),
+              (p + "0.SelfAttention.o.weight", (D, I), "fanin", 0.5)]
+        if l == 0:
+            s += [(p + "0.SelfAttention.relative_attention_bias.weight", (cfg.t_buckets, cfg.t_heads), "normal", 0.5)]
+        s += [(p + "0.layer_norm.weight", (D,), "gamma", 0.1)]
+        s += [(p + "1.DenseReluDense.wi_0.weight", (cfg.t_ff, D), "fanin", 1.0),
+              (p + "1.DenseReluDense.wi_1.weight", (cfg.t_ff, D), "fanin", 1.0),
+              (p + "1.DenseReluDense.wo.weight", (D, cfg.t_ff), "fanin", 0.5),
+              (p + "1.layer_norm.weight", (D,), "gamma", 0.1)]
+    s += [(tp + "encoder.final_layer_norm.weight", (D,), "gamma", 0.1)]
+    return s
+
+
+def text_state(seed: int = 0, cfg: TextConfig = TextConfig()) -> Dict[str, torch.Tensor]:
+    return make_state(text_specs(cfg), seed + 3)
+
+
 def synthetic_context(batch: int, seed0: int = 1000, tokens: int = 154, dim: int = 1024) -> torch.Tensor:
     """(B, 154, 1024) fp32 conditioning, prompt i seeded with ``seed0 + i``."""
     rows = [torch.randn((tokens, dim), generator=torch.Generator().manual_seed(seed0 + i)) for i in range(batch)]

@@ -230,9 +230,9 @@ typedef struct alcm_named_tensor {
 
 typedef struct alcm_model alcm_model;
 
-/* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL decoder, 2 = BigVGAN.
+/* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL decoder, 2 = BigVGAN, 3 = FrozenCLAPFLANEmbedder text encoders.
  * iconfig/fconfig: see DESIGN.md §C-ABI (hyper-parameters from configs/audiolcm.yaml / bigvgan json) */
-enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2 };
+enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2, ALCM_MODEL_TEXT = 3 };
 /* policy: ALCM_POLICY_* (below) */
 int alcm_model_create(int kind, const int* iconfig, int n_iconfig, const alcm_named_tensor* tensors,
                       int n_tensors, int policy, alcm_model** out);
@@ -270,6 +270,18 @@ int alcm_vae_decode(alcm_model* m, const float* z, float inv_scale_factor, float
 size_t alcm_bigvgan_workspace_bytes(const alcm_model* m, int B, int M);
 int alcm_bigvgan_forward(alcm_model* m, const float* mel, float* wav_out, int B, int M, void* ws,
                          size_t ws_bytes, alcm_stream_t stream);
+
+/* Text conditioning: FrozenCLAPFLANEmbedder.encode (ldm/modules/encoders/modules.py:567-582) from token ids.
+ * clap_ids / t5_ids (B, L) int64 DEVICE (the CLAP-BERT and T5 tokenizers' input_ids, L <= max_len = 77,
+ * ids in [0, vocab): out-of-range ids embed as zero rows) -> out (B, 2L, 1024) fp32 DEVICE =
+ * [Projection(BERT(clap_ids)) | T5Encoder(t5_ids)], no attention mask (as the reference).
+ * iconfig (14 ints): bert vocab, hidden, layers, heads, intermediate, max_position, projection out,
+ * t5 vocab, d_model, d_kv, heads, d_ff, layers, max_len.  Tensors: caption_encoder.base.* (BertModel),
+ * caption_encoder.projection.*, t5_transformer.* (T5EncoderModel) plus "_alcm.t5_rel_buckets" (max_len x
+ * max_len, the bidirectional relative-position bucket of j - i as float). */
+size_t alcm_text_workspace_bytes(const alcm_model* m, int B, int L);
+int alcm_text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5_ids, float* out, int B, int L,
+                     void* ws, size_t ws_bytes, alcm_stream_t stream);
 
 /* ---------------------------------------------------------------- live kernel timing (bench.py roofline)
  * Between begin/end every kernel launch is bracketed by hipEvents on its stream; end synchronises

@@ -378,3 +378,93 @@ def pcm16_bytes(wav: np.ndarray) -> bytes:
     x = np.asarray(wav, dtype=np.float32) * np.float32(32767.0)
     x = np.clip(np.rint(x), -32768, 32767).astype("<i2")
     return x.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# text conditioning  (FrozenCLAPFLANEmbedder.encode, ldm/modules/encoders/modules.py:567-582)
+# BERT (transformers BertModel, bert-base-uncased config), CLAP Projection (CLAP/clap.py:8-20) and the
+# T5 v1.1 encoder (transformers T5EncoderModel: T5LayerNorm = RMSNorm, unscaled attention + relative position
+# bias of block 0, gated-gelu FFN with gelu_new).  Third-party: transformers (5.15 here; the reference pins no
+# version, requirements.txt).  Pinned by tests/golden/text_B2_L77.npz from the reference encode() itself.
+# ---------------------------------------------------------------------------
+def t5_relative_bucket(L: int, num_buckets: int = 32, max_distance: int = 128) -> Tensor:
+    """``T5Attention._relative_position_bucket`` (bidirectional) of (j - i) for an L x L self-attention."""
+    rel = torch.arange(L)[None, :] - torch.arange(L)[:, None]
+    nb = num_buckets // 2
+    out = (rel > 0).long() * nb
+    rel = rel.abs()
+    exact = nb // 2
+    large = exact + (torch.log(rel.float() / exact) / math.log(max_distance / exact) * (nb - exact)).long()
+    large = torch.clamp(large, max=nb - 1)
+    return out + torch.where(rel < exact, rel, large)
+
+
+def _mha(q: Tensor, k: Tensor, v: Tensor, heads: int, scale: float, bias: Optional[Tensor] = None) -> Tensor:
+    B, L, I = q.shape
+    d = I // heads
+    q, k, v = (t.reshape(B, L, heads, d).permute(0, 2, 1, 3) for t in (q, k, v))
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if bias is not None:
+        s = s + bias
+    p = s.float().softmax(-1)
+    return torch.matmul(p, v).permute(0, 2, 1, 3).reshape(B, L, I)
+
+
+def bert_forward(W: W_t, ids: Tensor, layers: int, heads: int, eps: float = 1e-12,
+                 p: str = "caption_encoder.base.") -> Tensor:
+    """BertModel(input_ids).last_hidden_state: embeddings (word + position + token_type 0) -> LayerNorm, then
+    post-LN layers: x = LN(x + Wo attn(x)); x = LN(x + W2 gelu(W1 x))."""
+    B, L = ids.shape
+    x = (W[p + "embeddings.word_embeddings.weight"][ids] + W[p + "embeddings.position_embeddings.weight"][:L]
+         + W[p + "embeddings.token_type_embeddings.weight"][0])
+    H = x.shape[-1]
+    x = F.layer_norm(x, (H,), W[p + "embeddings.LayerNorm.weight"], W[p + "embeddings.LayerNorm.bias"], eps)
+    for l in range(layers):
+        q = f"{p}encoder.layer.{l}."
+        lin = lambda t, n: F.linear(t, W[q + n + ".weight"], W[q + n + ".bias"])
+        a = _mha(lin(x, "attention.self.query"), lin(x, "attention.self.key"), lin(x, "attention.self.value"),
+                 heads, (H // heads) ** -0.5)
+        x = F.layer_norm(lin(a, "attention.output.dense") + x, (H,), W[q + "attention.output.LayerNorm.weight"],
+                         W[q + "attention.output.LayerNorm.bias"], eps)
+        h = F.gelu(lin(x, "intermediate.dense"))
+        x = F.layer_norm(lin(h, "output.dense") + x, (H,), W[q + "output.LayerNorm.weight"],
+                         W[q + "output.LayerNorm.bias"], eps)
+    return x
+
+
+def clap_projection(W: W_t, x: Tensor, p: str = "caption_encoder.projection.") -> Tensor:
+    """CLAP/clap.py:16-20: LayerNorm(e1 + linear2(gelu(e1))), e1 = linear1(x); dropout = identity (eval)."""
+    e1 = F.linear(x, W[p + "linear1.weight"])
+    e2 = F.linear(F.gelu(e1), W[p + "linear2.weight"])
+    return F.layer_norm(e1 + e2, (e1.shape[-1],), W[p + "layer_norm.weight"], W[p + "layer_norm.bias"], 1e-5)
+
+
+def t5_encoder_forward(W: W_t, ids: Tensor, layers: int, heads: int, eps: float = 1e-6,
+                       p: str = "t5_transformer.") -> Tensor:
+    """T5EncoderModel(input_ids).last_hidden_state (v1.1): pre-RMSNorm blocks, unscaled attention + the
+    relative position bias of block 0, gated-gelu FFN (gelu_new(wi_0 h) * wi_1 h), final RMSNorm."""
+    B, L = ids.shape
+    x = W[p + "shared.weight"][ids]
+
+    def rms(t, w):
+        return w * (t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + eps))
+    tab = W[p + "encoder.block.0.layer.0.SelfAttention.relative_attention_bias.weight"]
+    bias = tab[t5_relative_bucket(L, tab.shape[0])].permute(2, 0, 1)[None]
+    for l in range(layers):
+        q = f"{p}encoder.block.{l}.layer."
+        h = rms(x, W[q + "0.layer_norm.weight"])
+        a = _mha(F.linear(h, W[q + "0.SelfAttention.q.weight"]), F.linear(h, W[q + "0.SelfAttention.k.weight"]),
+                 F.linear(h, W[q + "0.SelfAttention.v.weight"]), heads, 1.0, bias)
+        x = x + F.linear(a, W[q + "0.SelfAttention.o.weight"])
+        h = rms(x, W[q + "1.layer_norm.weight"])
+        g = F.gelu(F.linear(h, W[q + "1.DenseReluDense.wi_0.weight"]), approximate="tanh")
+        x = x + F.linear(g * F.linear(h, W[q + "1.DenseReluDense.wi_1.weight"]), W[q + "1.DenseReluDense.wo.weight"])
+    return rms(x, W[p + "encoder.final_layer_norm.weight"])
+
+
+def text_encode(W: W_t, clap_ids: Tensor, t5_ids: Tensor, bert_layers: int = 12, bert_heads: int = 12,
+                t5_layers: int = 24, t5_heads: int = 16) -> Tensor:
+    """FrozenCLAPFLANEmbedder.encode from token ids: concat([Projection(BERT), T5], dim=1) (modules.py:579-582)."""
+    z = clap_projection(W, bert_forward(W, clap_ids, bert_layers, bert_heads))
+    z2 = t5_encoder_forward(W, t5_ids, t5_layers, t5_heads)
+    return torch.cat([z, z2], dim=1)

@@ -58,6 +58,12 @@ def install_stubs():
     mod("taming", modules=m)
     mod("icecream", ic=print)
     mod("omegaconf", OmegaConf=object, ListConfig=list)
+    # the CLAP package imports its (unused) audio encoder's torchlibrosa front-end; modules.py imports
+    # importlib_resources.files (used only to read the CLAP config in __init__)
+    st = mod("torchlibrosa.stft", Spectrogram=object, LogmelFilterBank=object)
+    mod("torchlibrosa", stft=st)
+    import importlib.resources
+    mod("importlib_resources", files=importlib.resources.files)
 
 
 def digest(state):
@@ -89,10 +95,12 @@ def save(name, **arrays):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", default="", help="comma-separated fixture groups to (re)generate: base, c2, c4, c5 "
+    ap.add_argument("--only", default="", help="comma-separated fixture groups to (re)generate: base, c2, c4, c5, text "
                                                "(default: all)")
     args = ap.parse_args()
-    groups = set(filter(None, args.only.split(","))) or {"base", "c2", "c4", "c5"}
+    groups = set(filter(None, args.only.split(","))) or {"base", "c2", "c4", "c5", "text"}
+    if "text" in groups:  # load transformers' model modules before the stubs shadow torchvision
+        from transformers import BertConfig, BertModel, T5Config, T5EncoderModel  # noqa: F401
     install_stubs()
     sys.path.insert(0, args.ref)
     torch.set_num_threads(max(1, len(os.sched_getaffinity(0))))
@@ -139,6 +147,9 @@ def main():
     dit_keys = set(lcm.unet.diffusion_model.state_dict().keys())
     assert dit_keys == set(Sd.keys()), sorted(dit_keys ^ set(Sd.keys()))[:10]
 
+    if "text" in groups:
+        with torch.no_grad():
+            text_fixture()
     with torch.no_grad():
         smp = LCMSampler(lcm)
         smp.make_schedule(verbose=False)
@@ -199,6 +210,57 @@ def main():
             assert calls["i"] == S - 1
             save("e2e_cfg_S4_B2_T312.npz", x_T=xT, noise=noise, context_seed0=1000, uncond_seed0=900, cfg_scale=scale, latent=den,
                  mel=lcm.decode_first_stage(den))
+
+
+def text_fixture():
+    """FrozenCLAPFLANEmbedder.encode (ldm/modules/encoders/modules.py:567-582) run as the reference code itself on
+    transformers BertModel / T5EncoderModel built from the bert-base-uncased / t5-v1_1-large configs and the
+    reference CLAP Projection, all loaded with the recipe's text weights; the tokenizers (vocab files absent
+    offline) are replaced by fixed token ids, which encode() receives through stub tokenizer objects."""
+    from transformers import BertConfig, BertModel, T5Config, T5EncoderModel
+    from ldm.modules.encoders import modules
+    from ldm.modules.encoders.CLAP.clap import Projection
+    from audiolcm_amd.text_encoder import SyntheticTokenizer
+    cfg = recipe.TextConfig()
+    W = recipe.text_state(0, cfg)
+    bert = BertModel(BertConfig(vocab_size=cfg.b_vocab, hidden_size=cfg.b_hidden, num_hidden_layers=cfg.b_layers,
+                                num_attention_heads=cfg.b_heads, intermediate_size=cfg.b_inter,
+                                max_position_embeddings=cfg.b_maxpos, attn_implementation="eager")).eval()
+    t5 = T5EncoderModel(T5Config(vocab_size=cfg.t_vocab, d_model=cfg.t_d, d_kv=cfg.t_dkv, d_ff=cfg.t_ff,
+                                 num_layers=cfg.t_layers, num_heads=cfg.t_heads, feed_forward_proj="gated-gelu",
+                                 relative_attention_num_buckets=cfg.t_buckets,
+                                 relative_attention_max_distance=cfg.t_max_distance, layer_norm_epsilon=1e-6,
+                                 is_encoder_decoder=False, attn_implementation="eager")).eval()
+    proj = Projection(cfg.b_hidden, cfg.p_out).eval()
+    sub = lambda pre: {k[len(pre):]: v for k, v in W.items() if k.startswith(pre)}
+    for m, pre in ((bert, "caption_encoder.base."), (proj, "caption_encoder.projection."), (t5, "t5_transformer.")):
+        sd = sub(pre)
+        if m is t5:
+            sd["encoder.embed_tokens.weight"] = sd["shared.weight"]
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        assert not unexpected and not [k for k in missing if "position_ids" not in k], (missing, unexpected)
+    caps = ["A man is speaking while birds chirp in the background",
+            "Rain falls on a tin roof as thunder rumbles far away, and a dog barks twice near the door"]
+    struct = [f"<{c}& all>" for c in caps]
+    clap_ids = SyntheticTokenizer("bert", cfg.b_vocab)(caps, max_length=77)["input_ids"]
+    t5_ids = SyntheticTokenizer("t5", cfg.t_vocab)(struct, max_length=77)["input_ids"]
+
+    class Tok:
+        def __init__(self, ids):
+            self.ids = ids
+
+        def __call__(self, texts, **kw):
+            return {"input_ids": self.ids}
+
+    class Enc(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.base, self.projection = bert, proj
+
+    stub = types.SimpleNamespace(clap_tokenizer=Tok(clap_ids), t5_tokenizer=Tok(t5_ids), caption_encoder=Enc(),
+                                 t5_transformer=t5, max_length=77, device="cpu")
+    out = modules.FrozenCLAPFLANEmbedder.encode(stub, {"ori_caption": caps, "struct_caption": struct})
+    save("text_B2_L77.npz", clap_ids=clap_ids, t5_ids=t5_ids, out=out, digest=digest(W))
 
 
 def base_fixtures(lcm, smp, voc, scheduling_lcm, orig, meta, Activation1d, SnakeBeta):

@@ -1,0 +1,89 @@
+"""Text conditioning on the HIP path (alcm_text_encode through the C-ABI) vs the reference encode().
+
+tests/golden/text_B2_L77.npz is FrozenCLAPFLANEmbedder.encode (ldm/modules/encoders/modules.py:567-582) run by
+tests/golden/make_golden.py as the reference code on transformers' BertModel / T5EncoderModel and the reference
+CLAP Projection with the recipe's text weights; the oracle restatement is pinned to it on the CPU
+(tests/test_oracle_golden.py).  Tolerances (relative L2 of the (B, 154, 1024) conditioning): split (bf16x3)
+policy <= 1e-4; mixed policy (fp16 MFMA on the encoders' linears and attention) <= 3e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def enc():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from audiolcm_amd import _hip
+    from audiolcm_amd.text_encoder import CLAPT5TextEncoder
+    _hip.require_device(0)
+    return CLAPT5TextEncoder.from_recipe(0, split=True)
+
+
+def test_text_encode_split_matches_reference(enc):
+    g = golden("text_B2_L77.npz")
+    out = enc.encode_ids(torch.from_numpy(g["clap_ids"]), torch.from_numpy(g["t5_ids"])).cpu().numpy()
+    assert out.shape == (2, 154, 1024)
+    err = rel_l2(out, g["out"])
+    print(f"text split: {err:.2e} (clap half {rel_l2(out[:, :77], g['out'][:, :77]):.2e}, "
+          f"t5 half {rel_l2(out[:, 77:], g['out'][:, 77:]):.2e})")
+    assert err < 1e-4
+
+
+def test_text_encode_mixed_policy(enc):
+    g = golden("text_B2_L77.npz")
+    enc.set_split("mixed")
+    try:
+        out = enc.encode_ids(torch.from_numpy(g["clap_ids"]), torch.from_numpy(g["t5_ids"])).cpu().numpy()
+    finally:
+        enc.set_split(True)
+    err = rel_l2(out, g["out"])
+    print(f"text mixed: {err:.2e}")
+    assert err < 3e-3
+
+
+def test_text_encode_short_sequence_and_batch_invariance(enc, states_text):
+    """L = 20 (< max_length: the relative-bias sub-block) vs the oracle, and prompt 1 alone == in a batch of 3."""
+    from oracle import alcm_oracle as O
+    g = golden("text_B2_L77.npz")
+    a, b = torch.from_numpy(g["clap_ids"])[:, :20], torch.from_numpy(g["t5_ids"])[:, :20]
+    out = enc.encode_ids(a, b).cpu()
+    with torch.no_grad():
+        ref = O.text_encode(states_text, a, b)
+    assert rel_l2(out.numpy(), ref.numpy()) < 1e-4
+    a3, b3 = torch.cat([a, a.flip(0)]), torch.cat([b, b.flip(0)])
+    three = enc.encode_ids(a3[:3], b3[:3]).cpu()
+    assert rel_l2(three[1:2].numpy(), out[1:2].numpy()) < 1e-6
+
+
+def test_text_encode_rejects_bad_ids(enc):
+    ids = torch.zeros((1, 77), dtype=torch.long)
+    with pytest.raises(IndexError):
+        enc.encode_ids(ids + 30522, ids)
+    with pytest.raises(ValueError):
+        enc.encode_ids(torch.zeros((1, 78), dtype=torch.long), torch.zeros((1, 78), dtype=torch.long))
+
+
+def test_embedder_encode_captions(enc):
+    """FrozenCLAPFLANEmbedder.encode on caption dicts (synthetic tokenizer stand-in) == encode_ids of the
+    tokenizer's ids, (B, 154, 1024), finite."""
+    from audiolcm_amd.text_encoder import FrozenCLAPFLANEmbedder
+    emb = FrozenCLAPFLANEmbedder(weights_path=None, t5version=None, text_model=None)
+    emb.model = enc
+    caps = ["a dog barks", "rain falls on a tin roof"]
+    text = {"ori_caption": caps, "struct_caption": [f"<{c}& all>" for c in caps]}
+    c = emb.encode(text)
+    a, b = emb.tokenize(text["ori_caption"], text["struct_caption"])
+    assert c.shape == (2, 154, 1024) and torch.isfinite(c).all()
+    assert torch.equal(c, enc.encode_ids(a, b))
+
+
+@pytest.fixture(scope="module")
+def states_text():
+    from audiolcm_amd import recipe
+    return recipe.text_state(0)

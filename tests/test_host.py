@@ -176,7 +176,7 @@ def test_product_fails_loudly_without_library(monkeypatch):
 
 
 def test_yaml_instantiates_lcm_model_without_gpu():
-    from audiolcm_amd import config, lcm, models, conditioning
+    from audiolcm_amd import config, lcm, models, text_encoder
     cfg = config.load_config(os.path.join(REPO, "configs", "audiolcm.yaml"))
     m = config.instantiate_from_config(cfg.model, split=True)
     assert isinstance(m, lcm.LCM_audio)
@@ -184,7 +184,9 @@ def test_yaml_instantiates_lcm_model_without_gpu():
     assert m.unet.diffusion_model.cfg.hidden_size == 576 and m.unet.diffusion_model.cfg.depth == 4
     assert isinstance(m.first_stage_model, models.AutoencoderKL)
     assert m.first_stage_model.cfg.upsample_levels == (1,)
-    assert isinstance(m.cond_stage_model, conditioning.FrozenCLAPFLANEmbedder)
+    assert isinstance(m.cond_stage_model, text_encoder.FrozenCLAPFLANEmbedder)
+    assert isinstance(m.cond_stage_model.clap_tokenizer, text_encoder.SyntheticTokenizer)  # no vocab offline
+    assert not m.cond_stage_model.model.loaded
     assert not m.unet.diffusion_model.loaded
     with pytest.raises(RuntimeError):
         m.unet.diffusion_model.forward_cached(torch.zeros(1, 20, 8), torch.zeros(1), None, None)
@@ -211,3 +213,25 @@ def test_roofline_model_reproduces_survey():
     assert abs(dit["gflop"] - 150.6) < 0.5           # per sample-step
     assert abs(RL.summary(RL.vae_layers(1, 312))["gflop"] - 65.8) < 0.2
     assert abs(RL.summary(RL.bigvgan_layers(1, 624))["gflop"] - 1125.5) < 0.5
+
+
+def test_t5_relative_bucket_matches_transformers():
+    """The bucket table the HIP T5 encoder is packed with == transformers' own T5Attention rule."""
+    from transformers.models.t5.modeling_t5 import T5Attention
+    from audiolcm_amd.text_encoder import relative_position_bucket
+    for L in (7, 77, 300):
+        rel = torch.arange(L)[None, :] - torch.arange(L)[:, None]
+        ref = T5Attention._relative_position_bucket(rel, bidirectional=True, num_buckets=32, max_distance=128)
+        assert torch.equal(relative_position_bucket(L), ref)
+
+
+def test_synthetic_tokenizer_layout():
+    from audiolcm_amd.text_encoder import SyntheticTokenizer
+    b = SyntheticTokenizer("bert", 30522)(["A dog barks.", "a dog barks"], max_length=8)["input_ids"]
+    assert b.shape == (2, 8) and b[0, 0] == 101 and b[0, 5] == 102 and b[0, 6:].tolist() == [0, 0]
+    assert torch.equal(b[0, 1:4], b[1, 1:4])          # lower-cased words map to the same ids
+    t = SyntheticTokenizer("t5", 32128)(["<a dog& all>"], max_length=77)["input_ids"]
+    n = int((t[0] != 0).sum())
+    assert t[0, n - 1] == 1 and int(t.max()) < 32128  # </s> then padding
+    long = SyntheticTokenizer("bert", 30522)(["w " * 200], max_length=77)["input_ids"]
+    assert long.shape == (1, 77) and long[0, -1] == 102  # truncated, [SEP] kept
