@@ -23,6 +23,8 @@ TARGET_ALIASES: Dict[str, str] = {
     "vocoder.bigvgan.models.BigVGAN": "audiolcm_amd.models.BigVGAN",
     "ldm.modules.encoders.modules.FrozenCLAPFLANEmbedder": "audiolcm_amd.text_encoder.FrozenCLAPFLANEmbedder",
     "ldm.models.diffusion.scheduling_lcm.LCMSampler": "audiolcm_amd.lcm.LCMSampler",
+    "ldm.data.tsvdataset.TSVDatasetStruct": "audiolcm_amd.data.TSVDatasetStruct",
+    "ldm.data.tsvdataset.TSVDataset": "audiolcm_amd.data.TSVDataset",
 }
 # accepted but inert at inference (training-only components named by the YAML)
 INERT_TARGETS = {"torch.nn.Identity", "ldm.lr_scheduler.LambdaLinearScheduler"}

@@ -4,7 +4,8 @@
 generate 2-step LCM samples, vocode them and write PCM16 16 kHz WAVs to
 ``results/test/<prompt-with-dashes>_0.wav``, returning the (last) path like the reference.
 Prompts are batched (the reference loops at batch 1); everything on the path runs in the HIP
-library.  Checkpoints are read with safe loaders only (``weights_only=True`` / yaml.safe_load).
+library.  Checkpoints are read with safe loaders only (audiolcm_amd/ckpt.py: ``weights_only=True`` with inert
+placeholders for a Lightning checkpoint's non-tensor objects; yaml.safe_load).
 """
 from __future__ import annotations
 
@@ -15,6 +16,7 @@ import numpy as np
 import torch
 
 from . import recipe
+from .ckpt import load_checkpoint, state_dict_of
 from .config import instantiate_from_config, load_config
 from .lcm import LCM_audio, LCMSampler
 from .models import BigVGAN, VocoderBigVGAN
@@ -27,8 +29,7 @@ def load_model_from_config(config, ckpt: Optional[str] = None, verbose: bool = T
     model = instantiate_from_config(config.model, split=split)
     if ckpt:
         print(f"Loading model from {ckpt}")
-        pl_sd = torch.load(ckpt, map_location="cpu", weights_only=True)
-        model.load_state_dict(pl_sd["state_dict"], strict=False)
+        model.load_state_dict(state_dict_of(load_checkpoint(ckpt)), strict=False)
     elif synthetic_seed is not None:
         model.load_recipe(synthetic_seed)
     else:
@@ -108,8 +109,9 @@ def _build(config_path, model_path, vocoder_path, synthetic_seed, split):
 def AudioLCMBatchInfer(ori_prompts: List[str], config_path: str = "configs/audiolcm.yaml",
                        model_path: str = "./model/000184.ckpt", vocoder_path: str = "./model/vocoder",
                        batch_size: int = 32, synthetic_seed: Optional[int] = None, split: bool = True,
-                       outpath: str = "results/test") -> str:
-    """InferAPI.py:135-166. Returns the path of the last prompt's WAV."""
+                       outpath: str = "results/test", seed: Optional[int] = None) -> str:
+    """InferAPI.py:135-166. Returns the path of the last prompt's WAV.  ``seed``: per-prompt RNG seeds
+    seed + i (default None: the global device RNG, as the reference)."""
     prompts = [dict(ori_caption=p, struct_caption=struct_caption(p)) for p in ori_prompts]
     model, sampler, vocoder, orig_steps = _build(config_path, model_path, vocoder_path, synthetic_seed, split)
     os.makedirs(outpath, exist_ok=True)
@@ -118,13 +120,17 @@ def AudioLCMBatchInfer(ori_prompts: List[str], config_path: str = "configs/audio
     names = [wav_name_for(p["ori_caption"]) for p in prompts]
     with torch.no_grad():
         for lo in range(0, len(prompts), batch_size):
-            gen.gen_batch(prompts[lo:lo + batch_size], names[lo:lo + batch_size])
+            n = len(prompts[lo:lo + batch_size])
+            gen.gen_batch(prompts[lo:lo + batch_size], names[lo:lo + batch_size],
+                          seeds=None if seed is None else list(range(seed + lo, seed + lo + n)))
     print(f"Your samples are ready and waiting four you here: \n{outpath} \nEnjoy.")
     return os.path.join(outpath, names[-1] + "_0.wav")
 
 
 def AudioLCMInfer(ori_prompt: str, config_path: str = "configs/audiolcm.yaml",
                   model_path: str = "./model/000184.ckpt", vocoder_path: str = "./model/vocoder",
-                  synthetic_seed: Optional[int] = None, split: bool = True, outpath: str = "results/test") -> str:
+                  synthetic_seed: Optional[int] = None, split: bool = True, outpath: str = "results/test",
+                  seed: Optional[int] = None) -> str:
     """InferAPI.py:103-133."""
-    return AudioLCMBatchInfer([ori_prompt], config_path, model_path, vocoder_path, 1, synthetic_seed, split, outpath)
+    return AudioLCMBatchInfer([ori_prompt], config_path, model_path, vocoder_path, 1, synthetic_seed, split, outpath,
+                              seed)

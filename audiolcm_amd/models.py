@@ -232,7 +232,8 @@ class AutoencoderKL(_HipModel):
 
     def init_from_ckpt(self, path, ignore_keys=()):
         """AutoencoderKL.init_from_ckpt (autoencoder1d.py:42-52), safe loader only."""
-        sd = torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+        from .ckpt import load_checkpoint, state_dict_of
+        sd = state_dict_of(load_checkpoint(path))
         sd = {k: v for k, v in sd.items() if not any(k.startswith(ik) for ik in ignore_keys)}
         return self.load_state_dict(sd)
 
@@ -317,8 +318,8 @@ class VocoderBigVGAN:
     def __init__(self, ckpt_vocoder=None, device="cuda", split: bool = True, state=None, h=None):
         import yaml
         if state is None:
-            sd = torch.load(os.path.join(ckpt_vocoder, "best_netG.pt"), map_location="cpu", weights_only=True)
-            state = sd["generator"]
+            from .ckpt import load_checkpoint, state_dict_of
+            state = state_dict_of(load_checkpoint(os.path.join(ckpt_vocoder, "best_netG.pt")), "generator")
             with open(os.path.join(ckpt_vocoder, "args.yml")) as f:
                 h = yaml.safe_load(f)
         self.generator = BigVGAN(h, split=split).load_state_dict(state)

@@ -235,3 +235,70 @@ def test_synthetic_tokenizer_layout():
     assert t[0, n - 1] == 1 and int(t.max()) < 32128  # </s> then padding
     long = SyntheticTokenizer("bert", 30522)(["w " * 200], max_length=77)["input_ids"]
     assert long.shape == (1, 77) and long[0, -1] == 102  # truncated, [SEP] kept
+
+
+AUDIOCAPS_ROWS = (  # three rows of the reference's audiocaps_test_16000_struct.tsv (data), one name repeated
+    "name\tdataset\tori_cap\tmel_path\tcaption\taudio_path\n"
+    "Y7fmOlUlwoNg\taudiocaps\tConstant rattling noise and sharp vibrations\taudiocaps_mels/test/Y7fmOlUlwoNg_mel.npy\t"
+    "<constant rattling noise& all>@<sharp vibrations& all>\tdata/audiocaps/test/Y7fmOlUlwoNg.wav\n"
+    "Y6BJ455B1aAs\taudiocaps\tA rocket flies by followed by a loud explosion and fire crackling as a truck engine "
+    "runs idle\taudiocaps_mels/test/Y6BJ455B1aAs_mel.npy\t<rocket flying by& start>@<loud explosion& mid>@<fire "
+    "crackling& mid>@<truck engine idle& mid>\tdata/audiocaps/test/Y6BJ455B1aAs.wav\n"
+    "Y7fmOlUlwoNg\taudiocaps\tRattling and vibrating\taudiocaps_mels/test/Y7fmOlUlwoNg_mel.npy\t"
+    "<rattling& all>@<vibrating& all>\tdata/audiocaps/test/Y7fmOlUlwoNg.wav\n")
+
+
+def test_tsv_dataset_struct(tmp_path):
+    """ldm/data/tsvdataset.py TSVDatasetStruct: running _<num> suffix per repeated name, caption dict; absent mels
+    are None (generation needs captions only); instantiated through the YAML test_dataset target."""
+    from audiolcm_amd import config
+    tsv = tmp_path / "caps.tsv"
+    tsv.write_text(AUDIOCAPS_ROWS)
+    mel = np.arange(80 * 10, dtype=np.float32).reshape(80, 10)
+    (tmp_path / "audiocaps_mels" / "test").mkdir(parents=True)
+    np.save(tmp_path / "audiocaps_mels" / "test" / "Y6BJ455B1aAs_mel.npy", mel)
+    cfg = config.load_config(os.path.join(REPO, "configs", "audiolcm.yaml"))
+    d = dict(cfg["test_dataset"])
+    d["params"] = dict(d["params"], tsv_path=str(tsv))
+    ds = config.instantiate_from_config(d)
+    assert len(ds) == 3
+    names = [ds[i]["f_name"] for i in range(3)]
+    assert names == ["Y7fmOlUlwoNg_0", "Y6BJ455B1aAs_0", "Y7fmOlUlwoNg_1"]
+    assert ds[1]["caption"]["ori_caption"].startswith("A rocket") and ds[1]["caption"]["struct_caption"].startswith("<rocket")
+    assert ds[0]["image"] is None and ds[1]["image"].shape == (80, 624) and np.array_equal(ds[1]["image"][:, :10], mel)
+
+
+def test_cli_arguments_match_reference():
+    """scripts/txt2audio_for_lcm.py argument surface (reference :48-152) with the reference defaults."""
+    from audiolcm_amd.cli import parse_args
+    o = parse_args([])
+    assert (o.prompt_txt, o.sample_rate, o.test_dataset, o.outdir, o.ddim_steps, o.n_iter, o.H, o.W, o.n_samples,
+            o.scale, o.resume, o.vocoder_ckpt) == ("prompt.txt", 22050, "none", "outputs/txt2audio-samples", 100, 1, 20,
+                                                   312, 1, 5.0, "", "vocoder/logs/audioset")
+    o = parse_args(["--test-dataset", "audiocaps", "--ddim_steps", "2", "-r", "x.ckpt", "-b", "c.yaml",
+                    "--vocoder-ckpt", "bigvgan", "--sample_rate", "16000"])
+    assert o.test_dataset == "audiocaps" and o.ddim_steps == 2 and o.resume == "x.ckpt" and o.base == "c.yaml"
+
+
+class _HParams:  # stands in for a Lightning checkpoint's OmegaConf / Namespace hyper_parameters
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def test_checkpoint_loader_is_safe_and_keeps_tensors(tmp_path):
+    """A Lightning-shaped .ckpt with non-tensor objects (hyper_parameters object, callback class keys, optimizer
+    state) loads through torch.load(weights_only=True) with inert placeholders: tensors intact, no class of the
+    file imported or constructed."""
+    from audiolcm_amd.ckpt import OpaqueObject, load_checkpoint, state_dict_of
+    sd = {"unet.diffusion_model.proj_in.weight": torch.randn(4, 2, 5), "scale_factor": torch.tensor(0.5)}
+    ck = {"state_dict": sd, "hyper_parameters": _HParams(lr=1e-4, cfg={"a": 1}), "callbacks": {_HParams: {"k": 1}},
+          "epoch": 3, "optimizer_states": [{"state": {}, "param_groups": [{"lr": 1.0}]}]}
+    path = str(tmp_path / "m.ckpt")
+    torch.save(ck, path)
+    with pytest.raises(Exception):
+        torch.load(path, weights_only=True)   # the plain safe loader refuses such a file
+    out = load_checkpoint(path)
+    assert isinstance(out["hyper_parameters"], OpaqueObject) and type(out["hyper_parameters"]) is not _HParams
+    got = state_dict_of(out)
+    assert set(got) == set(sd) and all(torch.equal(got[k], sd[k]) for k in sd)
+    assert out["epoch"] == 3
