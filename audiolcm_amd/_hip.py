@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ALCM_LIB", os.path.join(HERE, "libaudiolcm_hip.so"))
 
 ALCM_OPND_ACT, ALCM_OPND_ACT_T, ALCM_OPND_WEIGHT = 0, 1, 2
-ALCM_MODEL_DIT, ALCM_MODEL_VAE, ALCM_MODEL_BIGVGAN, ALCM_MODEL_TEXT = 0, 1, 2, 3
+ALCM_MODEL_DIT, ALCM_MODEL_VAE, ALCM_MODEL_BIGVGAN, ALCM_MODEL_TEXT, ALCM_MODEL_MEL = 0, 1, 2, 3, 4
 ACT_NONE, ACT_SILU, ACT_GELU_ERF, ACT_GELU_TANH, ACT_TANH = 0, 1, 2, 3, 4
 PREC_BF16, PREC_SPLIT, PREC_F16, PREC_F16W2 = 0, 1, 2, 3   # per-launch MFMA operand precision
 POLICY_BF16, POLICY_SPLIT, POLICY_MIXED = 0, 1, 2      # per-model precision policy
@@ -98,6 +98,11 @@ _SIGS = [
     ("alcm_vae_decode", C.c_int, [vp, fp, C.c_float, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
     ("alcm_bigvgan_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_bigvgan_forward", C.c_int, [vp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+    ("alcm_vae_encode_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
+    ("alcm_vae_encode", C.c_int, [vp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
+    ("alcm_vae_encode_len", C.c_int, [vp, C.c_int]),
+    ("alcm_mel_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
+    ("alcm_mel_spectrogram", C.c_int, [vp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
     ("alcm_text_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_text_encode", C.c_int, [vp, vp, vp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
     ("alcm_profile_begin", C.c_int, [C.c_double, C.c_double]),

@@ -28,6 +28,11 @@ int set_error(int code, const std::string& msg) {
 
 int sincos_embedding(const float* v, float vscale, const float* freqs, int B, int half, int cos_first, float* out,
                      hipStream_t s);
+// alcm_mel.hip
+int reflect_pad_clamp(const float* x, int B, int L, int p, float* y, hipStream_t s);
+int stft_magnitude(const float* spec, int F, int64_t rows, float* mag, hipStream_t s);
+int log10_nct(const float* x, int B, int T, int C, float* out, hipStream_t s);
+int rows_stride2(const float* in, int B, int T, int To, int C, float* out, hipStream_t s);
 // alcm_text.hip
 int embed_gather(const int64_t* ids, int rows, const float* table, int64_t vocab, int D, const float* add, int L,
                  float* out, hipStream_t s);
@@ -73,7 +78,17 @@ struct ResW {
   bool has_nin = false;
   int cin = 0, cout = 0;
 };
+struct VaeEncW {  // Encoder1D + quant_conv (autoencoder1d.py:319-413, :31-33), present when encoder.* keys are
+  bool present = false;
+  int in_ch = 80;
+  ConvW conv_in, conv_out, quant, attn_qkv, attn_out;
+  std::vector<std::vector<ResW>> lv;  // lv[level]
+  std::vector<ConvW> down;            // down[level] (w.p == nullptr if none)
+  ResW mid1, mid2;
+  NormW attn_n, norm_out;
+};
 struct VaeW {
+  VaeEncW enc;
   int z_ch = 20, embed = 20, out_ch = 80, ksz = 5, ch = 384, nrb = 2;
   std::vector<int> mult;
   std::vector<int> up_levels;
@@ -82,6 +97,12 @@ struct VaeW {
   NormW attn_n, norm_out;
   std::vector<std::vector<ResW>> lv;  // lv[level]
   std::vector<ConvW> up;              // up[level] (w.p == nullptr if none)
+};
+
+struct MelW {  // log-mel front-end (NAT_mel.py:42-85): STFT as a GEMM over frames + mel projection
+  int n_fft = 1024, hop = 256, win = 1024, n_mels = 80, n_freq = 513;
+  ConvW dft;     // [2 n_freq][n_fft]: window * cos / -window * sin, K = tap * hop + c over n_fft / hop taps
+  ConvW basis;   // [n_mels][n_freq]
 };
 
 struct ActW {
@@ -148,6 +169,7 @@ struct alcm_model {
   alcm::VaeW vae;
   alcm::VocW voc;
   alcm::TextW text;
+  alcm::MelW mel;
   // BigVGAN: the three resblocks of a stage are independent chains until their mean; they run on the
   // caller's stream plus two auxiliary streams ordered by events, so the VALU / HBM bound Activation1d
   // kernels of one chain overlap the MFMA-bound convs of another.  The auxiliary streams and events belong
@@ -349,14 +371,14 @@ static void build_dit(Ingest& I, const int* ic, int nic) {
   D.fin = I.conv("final_layer.conv1d.", D.in_ch, H, 1);
 }
 
-static ResW build_res(Ingest& I, const std::string& p, int cin, int cout) {
+static ResW build_res(Ingest& I, const std::string& p, int cin, int cout, int k = 3) {
   ResW r;
   r.cin = cin;
   r.cout = cout;
   r.n1 = I.norm(p + "norm1.", cin);
-  r.c1 = I.conv(p + "conv1.", cout, cin, 3);
+  r.c1 = I.conv(p + "conv1.", cout, cin, k);
   r.n2 = I.norm(p + "norm2.", cout);
-  r.c2 = I.conv(p + "conv2.", cout, cout, 3);
+  r.c2 = I.conv(p + "conv2.", cout, cout, k);
   r.has_nin = cin != cout;
   if (r.has_nin) r.nin = I.conv(p + "nin_shortcut.", cout, cin, 1);
   return r;
@@ -411,6 +433,73 @@ static void build_vae(Ingest& I, const int* ic, int nic) {
   }
   V.norm_out = I.norm(d + "norm_out.", block_in);
   V.conv_out = I.conv(d + "conv_out.", V.out_ch, block_in, V.ksz);
+  // Encoder1D (the audio-to-latent direction): built when the checkpoint carries it
+  if (I.has("encoder.conv_in.weight")) {
+    VaeEncW& E = V.enc;
+    E.present = true;
+    const std::string e = "encoder.";
+    E.in_ch = (int)I.by.at(e + "conv_in.weight")->shape[1];
+    E.conv_in = I.conv(e + "conv_in.", V.ch, E.in_ch, V.ksz);
+    int bi = V.ch;
+    E.lv.assign(nl, {});
+    E.down.assign(nl, ConvW{});
+    for (int lvl = 0; lvl < nl; ++lvl) {
+      const int bo = V.ch * V.mult[lvl];
+      for (int ib = 0; ib < V.nrb; ++ib) {
+        E.lv[lvl].push_back(build_res(I, e + "down." + std::to_string(lvl) + ".block." + std::to_string(ib) + ".", bi,
+                                      bo, V.ksz));
+        bi = bo;
+      }
+      for (int u : V.up_levels)  // down_layers = up_levels - 1
+        if (u - 1 == lvl) E.down[lvl] = I.conv(e + "down." + std::to_string(lvl) + ".downsample.conv.", bi, bi, 3);
+    }
+    E.mid1 = build_res(I, e + "mid.block_1.", bi, bi, V.ksz);
+    {
+      const std::string a = e + "mid.attn_1.";
+      E.attn_n = I.norm(a + "norm.", bi);
+      std::vector<float> w, b;
+      for (const char* q : {"q", "k", "v"}) {
+        auto wq = I.get(a + q + ".weight", {bi, bi, 1});
+        auto bq = I.get(a + q + ".bias", {bi});
+        w.insert(w.end(), wq.begin(), wq.end());
+        b.insert(b.end(), bq.begin(), bq.end());
+      }
+      E.attn_qkv.w = I.pack(w, 3 * bi, bi, 1);
+      E.attn_qkv.b = I.upload(b);
+      E.attn_out = I.conv(a + "proj_out.", bi, bi, 1);
+    }
+    E.mid2 = build_res(I, e + "mid.block_2.", bi, bi, V.ksz);
+    E.norm_out = I.norm(e + "norm_out.", bi);
+    E.conv_out = I.conv(e + "conv_out.", 2 * V.z_ch, bi, V.ksz);
+    E.quant = I.conv("quant_conv.", 2 * V.embed, 2 * V.z_ch, 1);
+  }
+}
+
+static void build_mel(Ingest& I, const int* ic, int nic) {
+  MelW& Mw = I.m->mel;
+  if (nic >= 4) {
+    Mw.n_fft = ic[0]; Mw.hop = ic[1]; Mw.win = ic[2]; Mw.n_mels = ic[3];
+  }
+  Mw.n_freq = Mw.n_fft / 2 + 1;
+  if (Mw.n_fft % Mw.hop || (Mw.n_fft - Mw.hop) % 2 || Mw.win > Mw.n_fft || Mw.hop % 8)
+    throw Error(ALCM_E_INVALID, "mel: n_fft must be a multiple of hop, (n_fft - hop) even, win <= n_fft");
+  auto window = I.get("window", {Mw.win});
+  std::vector<float> wfull(Mw.n_fft, 0.f);  // torch.stft centres a shorter window inside n_fft
+  const int off = (Mw.n_fft - Mw.win) / 2;
+  for (int i = 0; i < Mw.win; ++i) wfull[off + i] = window[i];
+  // conv weight [co][ci][tap]: co = bin (re | im), ci = sample within a hop-row, tap = hop-row within the frame
+  const int taps = Mw.n_fft / Mw.hop, F = Mw.n_freq;
+  std::vector<float> w((size_t)2 * F * Mw.hop * taps);
+  for (int k = 0; k < F; ++k)
+    for (int c = 0; c < Mw.hop; ++c)
+      for (int t = 0; t < taps; ++t) {
+        const int n = t * Mw.hop + c;
+        const double ang = 2.0 * M_PI * (double)((int64_t)k * n % Mw.n_fft) / Mw.n_fft;
+        w[((size_t)k * Mw.hop + c) * taps + t] = (float)(wfull[n] * std::cos(ang));
+        w[((size_t)(F + k) * Mw.hop + c) * taps + t] = (float)(-wfull[n] * std::sin(ang));
+      }
+  Mw.dft.w = I.pack(w, 2 * F, Mw.hop, taps);
+  Mw.basis.w = I.pack(I.get("mel_basis", {Mw.n_mels, F}), Mw.n_mels, F, 1);
 }
 
 static ActW build_act(Ingest& I, const std::string& p, int C) {
@@ -576,6 +665,8 @@ static int conv(hipStream_t s, int split, int B, int rows_per_batch, const View&
   g.prec = split;
   return gemm(g, s);
 }
+
+static int lin(hipStream_t s, int prec, int R, const float* x, int C, const ConvW& w, float* y, const ConvOpts& o);
 
 struct Bump {
   char* base;
@@ -884,7 +975,7 @@ static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& 
     return plane_conv3(s, pk3, B, T, r.cout, w.pl, r.c2, resid, out);
   }
   ConvOpts o1;
-  o1.pad = 1;
+  o1.pad = r.c1.w.taps / 2;
   o1.pro = Pro{w.gsc, w.gsh, r.cin, nullptr, nullptr, ACT_SILU};
   ALCM_TRY(conv(s, pk3, B, T, cl(x, T, r.cin), r.c1, ocl(tmp, T, r.cout), o1));
   ALCM_TRY(group_norm_affine(tmp, B, T, r.cout, (int64_t)T * r.cout, r.cout, 32, 1e-6f, r.n2.g, r.n2.b, w.gsc, w.gsh, s));
@@ -894,11 +985,14 @@ static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& 
     resid = sc;
   }
   ConvOpts o2;
-  o2.pad = 1;
+  o2.pad = r.c2.w.taps / 2;
   o2.pro = Pro{w.gsc, w.gsh, r.cout, nullptr, nullptr, ACT_SILU};
   o2.res = Res{resid, (int64_t)T * r.cout, r.cout, 1};
   return conv(s, pk3, B, T, cl(tmp, T, r.cout), r.c2, ocl(out, T, r.cout), o2);
 }
+
+static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& nw, const ConvW& qkvw, const ConvW& ow,
+                    float* h, VaeWs& w);
 
 static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel, int B, int T, void* ws, size_t wsb,
                       hipStream_t s) {
@@ -925,41 +1019,7 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
   }
   float* h = w.a;
   ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid1, h, w.b, nullptr, h, w));
-  // AttnBlock1D (autoencoder1d.py:259-278): single head over T, logit scale C^-1/2
-  {
-    ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, V.attn_n.g, V.attn_n.b, w.gsc, w.gsh, s));
-    ConvOpts o;
-    o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, 0};
-    ALCM_TRY(conv(s, split, B, T, cl(h, T, C), V.attn_qkv, ocl(w.qkv, T, 3 * C), o));
-    const int Tp = round_up(T, 8);
-    alcm_gemm_args g;
-    std::memset(&g, 0, sizeof(g));
-    g.M = T; g.N = T; g.Kpad = round_up(C, kBK); g.batch = B; g.zdiv = 1;
-    g.a.kind = ALCM_OPND_ACT; g.a.ptr = w.qkv; g.a.st = 3 * C; g.a.sc = 1; g.a.T_in = T; g.a.C_in = C; g.a.Cpad = C;
-    g.a.ksize = 1; g.a.dil = 1; g.a.up = 1; g.a.rows_per_batch = T; g.a.zs1 = (int64_t)T * 3 * C;
-    g.b = g.a;
-    g.b.ptr = w.qkv + C;
-    g.acc_scale = 1.0f / sqrtf((float)C);
-    g.out_scale = 1.f;
-    g.out = w.S; g.o_st = Tp; g.o_sc = 1; g.o_zs1 = (int64_t)T * Tp; g.out_rows_per_batch = T; g.out_step = 1;
-    g.prec = split;
-    ALCM_TRY(gemm(g, s));
-    ALCM_TRY(softmax_rows(w.S, B * T, T, Tp, s));
-    alcm_gemm_args p;
-    std::memset(&p, 0, sizeof(p));
-    p.M = T; p.N = C; p.Kpad = round_up(Tp, kBK); p.batch = B; p.zdiv = 1;
-    p.a.kind = ALCM_OPND_ACT; p.a.ptr = w.S; p.a.st = Tp; p.a.sc = 1; p.a.T_in = T; p.a.C_in = Tp; p.a.Cpad = Tp;
-    p.a.ksize = 1; p.a.dil = 1; p.a.up = 1; p.a.rows_per_batch = T; p.a.zs1 = (int64_t)T * Tp;
-    p.b.kind = ALCM_OPND_ACT_T; p.b.ptr = w.qkv + 2 * C; p.b.st = 3 * C; p.b.sc = 1; p.b.T_in = T; p.b.rows = C;
-    p.b.zs1 = (int64_t)T * 3 * C;
-    p.acc_scale = 1.f; p.out_scale = 1.f;
-    p.out = w.c; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
-    p.prec = split;
-    ALCM_TRY(gemm(p, s));
-    ConvOpts oo;
-    oo.res = Res{h, (int64_t)T * C, C, 1};
-    ALCM_TRY(conv(s, split, B, T, cl(w.c, T, C), V.attn_out, ocl(h, T, C), oo));
-  }
+  ALCM_TRY(vae_attn(s, split, B, T, C, V.attn_n, V.attn_qkv, V.attn_out, h, w));
   ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid2, h, w.b, nullptr, h, w));
   int Tc = T;
   float* spare = w.c;  // third full buffer for channel-changing blocks
@@ -994,6 +1054,133 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
   o.pad = V.ksz / 2;
   o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, ACT_SILU};
   return conv(s, split, B, Tc, cl(h, Tc, C), V.conv_out, Out{mel, (int64_t)V.out_ch * Tc, 1, Tc, 1, 0}, o);
+}
+
+// AttnBlock1D (autoencoder1d.py:259-278): single head over T, logit scale C^-1/2; h += proj_out(attn(GN(h)))
+static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& nw, const ConvW& qkvw, const ConvW& ow,
+                    float* h, VaeWs& w) {
+  {
+    ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, nw.g, nw.b, w.gsc, w.gsh, s));
+    ConvOpts o;
+    o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, 0};
+    ALCM_TRY(conv(s, split, B, T, cl(h, T, C), qkvw, ocl(w.qkv, T, 3 * C), o));
+    const int Tp = round_up(T, 8);
+    alcm_gemm_args g;
+    std::memset(&g, 0, sizeof(g));
+    g.M = T; g.N = T; g.Kpad = round_up(C, kBK); g.batch = B; g.zdiv = 1;
+    g.a.kind = ALCM_OPND_ACT; g.a.ptr = w.qkv; g.a.st = 3 * C; g.a.sc = 1; g.a.T_in = T; g.a.C_in = C; g.a.Cpad = C;
+    g.a.ksize = 1; g.a.dil = 1; g.a.up = 1; g.a.rows_per_batch = T; g.a.zs1 = (int64_t)T * 3 * C;
+    g.b = g.a;
+    g.b.ptr = w.qkv + C;
+    g.acc_scale = 1.0f / sqrtf((float)C);
+    g.out_scale = 1.f;
+    g.out = w.S; g.o_st = Tp; g.o_sc = 1; g.o_zs1 = (int64_t)T * Tp; g.out_rows_per_batch = T; g.out_step = 1;
+    g.prec = split;
+    ALCM_TRY(gemm(g, s));
+    ALCM_TRY(softmax_rows(w.S, B * T, T, Tp, s));
+    alcm_gemm_args p;
+    std::memset(&p, 0, sizeof(p));
+    p.M = T; p.N = C; p.Kpad = round_up(Tp, kBK); p.batch = B; p.zdiv = 1;
+    p.a.kind = ALCM_OPND_ACT; p.a.ptr = w.S; p.a.st = Tp; p.a.sc = 1; p.a.T_in = T; p.a.C_in = Tp; p.a.Cpad = Tp;
+    p.a.ksize = 1; p.a.dil = 1; p.a.up = 1; p.a.rows_per_batch = T; p.a.zs1 = (int64_t)T * Tp;
+    p.b.kind = ALCM_OPND_ACT_T; p.b.ptr = w.qkv + 2 * C; p.b.st = 3 * C; p.b.sc = 1; p.b.T_in = T; p.b.rows = C;
+    p.b.zs1 = (int64_t)T * 3 * C;
+    p.acc_scale = 1.f; p.out_scale = 1.f;
+    p.out = w.c; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
+    p.prec = split;
+    ALCM_TRY(gemm(p, s));
+    ConvOpts oo;
+    oo.res = Res{h, (int64_t)T * C, C, 1};
+    ALCM_TRY(conv(s, split, B, T, cl(w.c, T, C), ow, ocl(h, T, C), oo));
+  }
+  return 0;
+}
+
+// Encoder1D + quant_conv (autoencoder1d.py:319-413, AutoencoderKL.encode :54-58): mel (B, in_ch, M) NCT ->
+// moments (B, 2 embed, To) NCT, To = M / 2^len(down_layers); DiagonalGaussianDistribution is host-side
+static int vae_encode(alcm_model* m, const float* x, float* moments, int B, int M, void* ws, size_t wsb,
+                      hipStream_t s) {
+  const VaeW& V = m->vae;
+  const VaeEncW& E = V.enc;
+  if (!E.present) return set_error(ALCM_E_MISSING, "vae_encode: the model was created without encoder.* weights");
+  const int split = prec_of(m, false);
+  const int pk = prec_of(m, true);
+  if (B <= 0 || M <= 1) return set_error(ALCM_E_INVALID, "vae_encode: bad shape");
+  Bump bp(ws, wsb);
+  VaeWs w = plan_vae(V, bp, B, M);
+  if (!ws || bp.off > wsb) return set_error(ALCM_E_WORKSPACE, "vae_encode: workspace too small");
+  int C = V.ch, T = M;
+  {
+    ConvOpts o;
+    o.pad = V.ksz / 2;
+    ALCM_TRY(conv(s, split, B, T, View{x, (int64_t)E.in_ch * T, 1, T, T, E.in_ch}, E.conv_in, ocl(w.a, T, C), o));
+  }
+  float* h = w.a;
+  float* spare = w.c;
+  for (size_t lvl = 0; lvl < E.lv.size(); ++lvl) {
+    for (const ResW& r : E.lv[lvl]) {
+      if (r.has_nin) {
+        ALCM_TRY(vae_res(s, split, pk, B, T, r, h, w.b, w.d, spare, w));
+        std::swap(h, spare);
+      } else {
+        ALCM_TRY(vae_res(s, split, pk, B, T, r, h, w.b, nullptr, h, w));
+      }
+      C = r.cout;
+    }
+    if (E.down[lvl].w.p) {
+      // Downsample1D (autoencoder1d.py:310-317): zero pad (0, 1), conv k3 stride 2 = the stride-1 conv (pad 0;
+      // rows past T read zeros) at even rows
+      const int To = (T - 2) / 2 + 1;
+      ALCM_TRY(conv(s, split, B, T, cl(h, T, C), E.down[lvl], ocl(w.b, T, C), ConvOpts{}));
+      ALCM_TRY(rows_stride2(w.b, B, T, To, C, spare, s));
+      std::swap(h, spare);
+      T = To;
+    }
+  }
+  ALCM_TRY(vae_res(s, split, pk, B, T, E.mid1, h, w.b, nullptr, h, w));
+  ALCM_TRY(vae_attn(s, split, B, T, C, E.attn_n, E.attn_qkv, E.attn_out, h, w));
+  ALCM_TRY(vae_res(s, split, pk, B, T, E.mid2, h, w.b, nullptr, h, w));
+  ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, E.norm_out.g, E.norm_out.b, w.gsc, w.gsh, s));
+  {
+    ConvOpts o;
+    o.pad = V.ksz / 2;
+    o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, ACT_SILU};
+    ALCM_TRY(conv(s, split, B, T, cl(h, T, C), E.conv_out, ocl(spare, T, 2 * V.z_ch), o));
+  }
+  return conv(s, split, B, T, cl(spare, T, 2 * V.z_ch), E.quant, Out{moments, (int64_t)2 * V.embed * T, 1, T, 1, 0},
+              ConvOpts{});
+}
+
+// log-mel spectrogram (MelNet.forward, NAT_mel.py:66-85, center=False): clamp(-1, 1), reflect pad (n_fft - hop)/2,
+// |STFT| (hann window, onesided) -> mel_basis @ mag -> log10(clamp(1e-5)); wav (B, L), L % hop == 0 -> (B, n_mels, L/hop)
+struct MelWs {
+  float *ypad, *spec, *mag, *mel;
+};
+static MelWs plan_mel(const MelW& Mw, Bump& bp, int B, int L) {
+  const size_t Fr = (size_t)L / Mw.hop;
+  MelWs w;
+  w.ypad = bp.take<float>((size_t)B * (L + Mw.n_fft - Mw.hop) + 64);
+  w.spec = bp.take<float>((size_t)B * Fr * 2 * Mw.n_freq);
+  w.mag = bp.take<float>((size_t)B * Fr * Mw.n_freq);
+  w.mel = bp.take<float>((size_t)B * Fr * Mw.n_mels);
+  return w;
+}
+static int mel_forward(alcm_model* m, const float* wav, float* mel, int B, int L, void* ws, size_t wsb, hipStream_t s) {
+  const MelW& Mw = m->mel;
+  if (B <= 0 || L <= 0 || L % Mw.hop || L <= (Mw.n_fft - Mw.hop) / 2)
+    return set_error(ALCM_E_INVALID, "mel_spectrogram: the waveform length must be a positive multiple of hop");
+  Bump bp(ws, wsb);
+  MelWs w = plan_mel(Mw, bp, B, L);
+  if (!ws || bp.off > wsb) return set_error(ALCM_E_WORKSPACE, "mel_spectrogram: workspace too small");
+  const int p = (Mw.n_fft - Mw.hop) / 2, Lp = L + 2 * p, rows = Lp / Mw.hop, Fr = L / Mw.hop, F = Mw.n_freq;
+  const int prec = m->policy == ALCM_POLICY_BF16 ? PREC_BF16 : PREC_SPLIT;  // log-magnitudes: keep fp32 accuracy
+  ALCM_TRY(reflect_pad_clamp(wav, B, L, p, w.ypad, s));
+  // frame f = padded samples [f hop, f hop + n_fft) = hop-rows f .. f + n_fft/hop - 1: a conv over the rows
+  ALCM_TRY(conv(s, prec, B, Fr, View{w.ypad, (int64_t)Lp, Mw.hop, 1, rows, Mw.hop}, Mw.dft,
+                ocl(w.spec, Fr, 2 * F), ConvOpts{}));
+  ALCM_TRY(stft_magnitude(w.spec, F, (int64_t)B * Fr, w.mag, s));
+  ALCM_TRY(lin(s, prec, B * Fr, w.mag, F, Mw.basis, w.mel, ConvOpts{}));
+  return log10_nct(w.mel, B, Fr, Mw.n_mels, mel, s);
 }
 
 // ------------------------------------------------------------------ BigVGAN
@@ -1463,6 +1650,7 @@ extern "C" int alcm_model_create(int kind, const int* iconfig, int n_iconfig, co
     else if (kind == ALCM_MODEL_VAE) build_vae(I, iconfig, n_iconfig);
     else if (kind == ALCM_MODEL_BIGVGAN) build_voc(I, iconfig, n_iconfig);
     else if (kind == ALCM_MODEL_TEXT) build_text(I, iconfig, n_iconfig);
+    else if (kind == ALCM_MODEL_MEL) build_mel(I, iconfig, n_iconfig);
     else throw Error(ALCM_E_INVALID, "unknown model kind");
     if (hipDeviceSynchronize() != hipSuccess) throw Error(ALCM_E_HIP, "device sync after weight upload failed");
   } catch (const Error& e) {
@@ -1571,4 +1759,38 @@ extern "C" int alcm_text_encode(alcm_model* m, const int64_t* clap_ids, const in
     return set_error(ALCM_E_INVALID, "text_encode: bad args");
   if (m->text.p_out != m->text.t_d) return set_error(ALCM_E_INVALID, "text_encode: projection and T5 widths differ");
   return text_encode(m, clap_ids, t5_ids, out, B, L, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" size_t alcm_vae_encode_workspace_bytes(const alcm_model* m, int B, int M) {
+  if (!m || m->kind != ALCM_MODEL_VAE) return 0;
+  Bump bp(nullptr, 0);
+  plan_vae(m->vae, bp, B, M);
+  return bp.off + 256;
+}
+
+extern "C" int alcm_vae_encode(alcm_model* m, const float* mel, float* moments_out, int B, int M, void* ws,
+                               size_t ws_bytes, alcm_stream_t stream) {
+  if (!m || m->kind != ALCM_MODEL_VAE || !mel || !moments_out) return set_error(ALCM_E_INVALID, "vae_encode: bad args");
+  return vae_encode(m, mel, moments_out, B, M, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int alcm_vae_encode_len(const alcm_model* m, int M) {
+  if (!m || m->kind != ALCM_MODEL_VAE) return -1;
+  int T = M;
+  for (const auto& d : m->vae.enc.down)
+    if (d.w.p) T = (T - 2) / 2 + 1;
+  return T;
+}
+
+extern "C" size_t alcm_mel_workspace_bytes(const alcm_model* m, int B, int L) {
+  if (!m || m->kind != ALCM_MODEL_MEL) return 0;
+  Bump bp(nullptr, 0);
+  plan_mel(m->mel, bp, B, L);
+  return bp.off + 256;
+}
+
+extern "C" int alcm_mel_spectrogram(alcm_model* m, const float* wav, float* mel_out, int B, int L, void* ws,
+                                    size_t ws_bytes, alcm_stream_t stream) {
+  if (!m || m->kind != ALCM_MODEL_MEL || !wav || !mel_out) return set_error(ALCM_E_INVALID, "mel: bad args");
+  return mel_forward(m, wav, mel_out, B, L, ws, ws_bytes, (hipStream_t)stream);
 }

@@ -104,6 +104,21 @@ class LCM_audio:
     def decode_first_stage(self, z):
         return self.first_stage_model.decode(z, self.scale_factor)
 
+    def encode_first_stage(self, x):
+        """lcm_audio.py:425-427: mel (B, 80, M) -> DiagonalGaussianDistribution over the latent."""
+        return self.first_stage_model.encode(x)
+
+    def get_first_stage_encoding(self, encoder_posterior, generator=None):
+        """lcm_audio.py:197-204: scale_factor * posterior.sample() (a tensor passes through)."""
+        from .models import DiagonalGaussianDistribution
+        if isinstance(encoder_posterior, DiagonalGaussianDistribution):
+            z = encoder_posterior.sample(generator)
+        elif isinstance(encoder_posterior, torch.Tensor):
+            z = encoder_posterior
+        else:
+            raise NotImplementedError(f"encoder_posterior of type '{type(encoder_posterior)}' not yet implemented")
+        return self.scale_factor * z
+
     def eval(self):
         return self
 

@@ -238,8 +238,31 @@ class AutoencoderKL(_HipModel):
         return self.load_state_dict(sd)
 
     def load_state_dict(self, state, strict=False):
-        keep = {k: v for k, v in state.items() if k.startswith("decoder.") or k.startswith("post_quant_conv.")}
+        keep = {k: v for k, v in state.items() if k.startswith("decoder.") or k.startswith("post_quant_conv.")
+                or k.startswith("encoder.") or k.startswith("quant_conv.")}
         return super().load_state_dict(keep, strict)
+
+    def encode(self, x: torch.Tensor) -> "DiagonalGaussianDistribution":
+        """AutoencoderKL.encode (autoencoder1d.py:54-58): Encoder1D + quant_conv on (B, 80, M) -> posterior over
+        (B, embed_dim, M / 2) latents (needs a checkpoint / recipe with the encoder.* weights)."""
+        self._need()
+        B, Cm, M = x.shape
+        x = x.contiguous().float()
+        To = int(lib().alcm_vae_encode_len(self._handle, M))
+        moments = torch.empty((B, 2 * self.cfg.embed_dim, To), device=x.device, dtype=torch.float32)
+        nb = int(lib().alcm_vae_encode_workspace_bytes(self._handle, B, M))
+        ws = self._workspace(("enc", B, M), nb, x.device)
+        check(lib().alcm_vae_encode(self._handle, ptr(x), ptr(moments), B, M, ptr(ws), ws.numel(), stream_handle()),
+              "alcm_vae_encode")
+        return DiagonalGaussianDistribution(moments)
+
+    def forward(self, input: torch.Tensor, sample_posterior: bool = True, generator=None):
+        """autoencoder1d.py:64-70: (reconstruction, posterior)."""
+        posterior = self.encode(input)
+        z = posterior.sample(generator) if sample_posterior else posterior.mode()
+        return self.decode(z), posterior
+
+    __call__ = forward
 
     def decode(self, z: torch.Tensor, scale_factor: float = 1.0) -> torch.Tensor:
         """post_quant_conv + Decoder1D on (B, 20, T) -> mel (B, 80, 2T); z is divided by scale_factor first."""
@@ -256,6 +279,29 @@ class AutoencoderKL(_HipModel):
     @classmethod
     def from_recipe(cls, seed: int = 0, split: bool = True) -> "AutoencoderKL":
         return cls(split=split).load_state_dict(recipe.vae_state(seed))
+
+
+class DiagonalGaussianDistribution:
+    """ldm/modules/distributions/distributions.py:24-44 over the encoder's (B, 2C, T) moments (device tensors):
+    mean | logvar split, logvar clamped to [-30, 20]; sample() draws the noise from `generator` (a torch
+    Generator on the device) or the global device RNG."""
+
+    def __init__(self, parameters: torch.Tensor, deterministic: bool = False):
+        self.parameters = parameters
+        self.mean, self.logvar = torch.chunk(parameters, 2, dim=1)
+        self.logvar = torch.clamp(self.logvar, -30.0, 20.0)
+        self.deterministic = deterministic
+        self.std = torch.exp(0.5 * self.logvar)
+        self.var = torch.exp(self.logvar)
+        if deterministic:
+            self.var = self.std = torch.zeros_like(self.mean)
+
+    def sample(self, generator=None) -> torch.Tensor:
+        eps = torch.randn(self.mean.shape, generator=generator, device=self.parameters.device)
+        return self.mean + self.std * eps
+
+    def mode(self) -> torch.Tensor:
+        return self.mean
 
 
 class BigVGAN(_HipModel):

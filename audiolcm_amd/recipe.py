@@ -201,6 +201,42 @@ def vae_decoder_specs(cfg: VAEConfig = VAEConfig()) -> List[Spec]:
     return s
 
 
+def vae_encoder_specs(cfg: VAEConfig = VAEConfig(), in_channels: int = 80) -> List[Spec]:
+    """Encode-path keys of ``AutoencoderKL.state_dict()``: ``encoder.*`` (Encoder1D, autoencoder1d.py:319-413:
+    its ResnetBlock1D convs use ddconfig kernel_size) and ``quant_conv`` (2 z -> 2 embed, :31-33)."""
+    s: List[Spec] = []
+    e, k = "encoder.", cfg.kernel_size
+    s += _conv(e + "conv_in.", cfg.ch, in_channels, k)
+    block_in = cfg.ch
+    for lvl, mult in enumerate(cfg.ch_mult):
+        block_out = cfg.ch * mult
+        for ib in range(cfg.num_res_blocks):
+            p = f"{e}down.{lvl}.block.{ib}."
+            s += _norm(p + "norm1.", block_in)
+            s += _conv(p + "conv1.", block_out, block_in, k)
+            s += _norm(p + "norm2.", block_out)
+            s += _conv(p + "conv2.", block_out, block_out, k, gain=0.5)
+            if block_in != block_out:
+                s += _conv(p + "nin_shortcut.", block_out, block_in, 1)
+            block_in = block_out
+        if lvl in cfg.down_layers:
+            s += _conv(f"{e}down.{lvl}.downsample.conv.", block_in, block_in, 3)
+    for b in ("mid.block_1.", "mid.block_2."):
+        s += _norm(e + b + "norm1.", block_in)
+        s += _conv(e + b + "conv1.", block_in, block_in, k)
+        s += _norm(e + b + "norm2.", block_in)
+        s += _conv(e + b + "conv2.", block_in, block_in, k, gain=0.5)
+    a = e + "mid.attn_1."
+    s += _norm(a + "norm.", block_in)
+    for q in ("q", "k", "v"):
+        s += _conv(f"{a}{q}.", block_in, block_in, 1)
+    s += _conv(a + "proj_out.", block_in, block_in, 1, gain=0.5)
+    s += _norm(e + "norm_out.", block_in)
+    s += _conv(e + "conv_out.", 2 * cfg.z_channels, block_in, k)
+    s += _conv("quant_conv.", 2 * cfg.embed_dim, 2 * cfg.z_channels, 1)
+    return s
+
+
 def _wn_conv(p: str, c_out: int, c_in: int, k: int, transposed: bool = False, gain: float = 1.0) -> List[Spec]:
     # weight_norm(dim=0): weight_g has shape (dim0, 1, 1)
     if transposed:
@@ -311,6 +347,10 @@ def dit_state(seed: int = 0, cfg: DiTConfig = DiTConfig()) -> Dict[str, torch.Te
 
 def vae_state(seed: int = 0, cfg: VAEConfig = VAEConfig()) -> Dict[str, torch.Tensor]:
     return make_state(vae_decoder_specs(cfg), seed + 1)
+
+
+def vae_encoder_state(seed: int = 0, cfg: VAEConfig = VAEConfig()) -> Dict[str, torch.Tensor]:
+    return make_state(vae_encoder_specs(cfg), seed + 1)
 
 
 def bigvgan_state(seed: int = 0, cfg: BigVGANConfig = BigVGANConfig()) -> Dict[str, torch.Tensor]:

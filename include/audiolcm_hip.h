@@ -230,9 +230,10 @@ typedef struct alcm_named_tensor {
 
 typedef struct alcm_model alcm_model;
 
-/* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL decoder, 2 = BigVGAN, 3 = FrozenCLAPFLANEmbedder text encoders.
+/* kind: 0 = ConcatDiT2MLP, 1 = AutoencoderKL (decoder; + Encoder1D when encoder.* tensors are given), 2 = BigVGAN,
+ * 3 = FrozenCLAPFLANEmbedder text encoders, 4 = log-mel front-end (NAT_mel.MelNet).
  * iconfig/fconfig: see DESIGN.md §C-ABI (hyper-parameters from configs/audiolcm.yaml / bigvgan json) */
-enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2, ALCM_MODEL_TEXT = 3 };
+enum { ALCM_MODEL_DIT = 0, ALCM_MODEL_VAE = 1, ALCM_MODEL_BIGVGAN = 2, ALCM_MODEL_TEXT = 3, ALCM_MODEL_MEL = 4 };
 /* policy: ALCM_POLICY_* (below) */
 int alcm_model_create(int kind, const int* iconfig, int n_iconfig, const alcm_named_tensor* tensors,
                       int n_tensors, int policy, alcm_model** out);
@@ -265,6 +266,22 @@ int alcm_dit_forward(alcm_model* m, const float* x, const int64_t* t, const floa
 size_t alcm_vae_workspace_bytes(const alcm_model* m, int B, int T);
 int alcm_vae_decode(alcm_model* m, const float* z, float inv_scale_factor, float* mel_out, int B, int T,
                     void* ws, size_t ws_bytes, alcm_stream_t stream);
+
+/* VAE encode_first_stage (AutoencoderKL.encode, autoencoder1d.py:54-58 -> Encoder1D :319-413 + quant_conv):
+ * mel (B,80,M) NCT -> posterior moments (B, 2*embed_dim, To) NCT = [mean | logvar] before the clamp,
+ * To = alcm_vae_encode_len(m, M) (M/2 for audiolcm.yaml).  Needs a model created with encoder.* tensors. */
+size_t alcm_vae_encode_workspace_bytes(const alcm_model* m, int B, int M);
+int alcm_vae_encode(alcm_model* m, const float* mel, float* moments_out, int B, int M, void* ws, size_t ws_bytes,
+                    alcm_stream_t stream);
+int alcm_vae_encode_len(const alcm_model* m, int M);
+
+/* Log-mel front-end (ldm/data/preprocess/NAT_mel.py:66-85, MelNet.forward with center=False): wav (B, L) fp32,
+ * L % hop == 0 -> mel (B, n_mels, L/hop) NCT = log10(clamp(mel_basis @ |STFT(reflect_pad(clamp(wav)))|, 1e-5)).
+ * Model kind ALCM_MODEL_MEL, iconfig {n_fft, hop, win, n_mels}, tensors "window" (win) and "mel_basis"
+ * (n_mels, n_fft/2+1). */
+size_t alcm_mel_workspace_bytes(const alcm_model* m, int B, int L);
+int alcm_mel_spectrogram(alcm_model* m, const float* wav, float* mel_out, int B, int L, void* ws, size_t ws_bytes,
+                         alcm_stream_t stream);
 
 /* BigVGAN. mel (B,80,M) NCT -> wav (B,1,256*M) */
 size_t alcm_bigvgan_workspace_bytes(const alcm_model* m, int B, int M);

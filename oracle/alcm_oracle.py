@@ -230,9 +230,10 @@ def _swish(x: Tensor) -> Tensor:
 def _resnet_block(W: W_t, p: str, x: Tensor) -> Tensor:
     """``ResnetBlock1D.forward`` without temb (autoencoder1d.py:212-235)."""
     h = _swish(F.group_norm(x, 32, W[p + "norm1.weight"], W[p + "norm1.bias"], 1e-6))
-    h = F.conv1d(h, W[p + "conv1.weight"], W[p + "conv1.bias"], padding=1)
+    k = W[p + "conv1.weight"].shape[-1]  # 3 in Decoder1D, ddconfig kernel_size (5) in Encoder1D
+    h = F.conv1d(h, W[p + "conv1.weight"], W[p + "conv1.bias"], padding=k // 2)
     h = _swish(F.group_norm(h, 32, W[p + "norm2.weight"], W[p + "norm2.bias"], 1e-6))
-    h = F.conv1d(h, W[p + "conv2.weight"], W[p + "conv2.bias"], padding=1)
+    h = F.conv1d(h, W[p + "conv2.weight"], W[p + "conv2.bias"], padding=k // 2)
     if (p + "nin_shortcut.weight") in W:
         x = F.conv1d(x, W[p + "nin_shortcut.weight"], W[p + "nin_shortcut.bias"])
     return x + h
@@ -272,6 +273,40 @@ def vae_decode(W: W_t, z: Tensor, scale_factor: float = 1.0, num_levels: int = 3
     h = _swish(F.group_norm(h, 32, W[d + "norm_out.weight"], W[d + "norm_out.bias"], 1e-6))
     k = W[d + "conv_out.weight"].shape[-1]
     return F.conv1d(h, W[d + "conv_out.weight"], W[d + "conv_out.bias"], padding=k // 2)
+
+
+def vae_encode_moments(W: W_t, x: Tensor, num_levels: int = 3, num_res_blocks: int = 2,
+                       down_layers: Sequence[int] = (0,)) -> Tensor:
+    """``AutoencoderKL.encode`` up to the posterior parameters (autoencoder1d.py:54-58): Encoder1D.forward
+    (:388-413: conv_in, per level num_res_blocks ResnetBlock1D (+ Downsample1D: zero pad (0, 1), conv k3
+    stride 2), mid block / attn / block, GN + swish + conv_out) -> quant_conv.  (B,80,M) -> (B,40,M/2)."""
+    e = "encoder."
+    k = W[e + "conv_in.weight"].shape[-1]
+    h = F.conv1d(x, W[e + "conv_in.weight"], W[e + "conv_in.bias"], padding=k // 2)
+    for lvl in range(num_levels):
+        for ib in range(num_res_blocks):
+            h = _resnet_block(W, f"{e}down.{lvl}.block.{ib}.", h)
+        if lvl in down_layers:
+            h = F.conv1d(F.pad(h, (0, 1)), W[f"{e}down.{lvl}.downsample.conv.weight"],
+                         W[f"{e}down.{lvl}.downsample.conv.bias"], stride=2)
+    h = _resnet_block(W, e + "mid.block_1.", h)
+    h = _attn_block(W, e + "mid.attn_1.", h)
+    h = _resnet_block(W, e + "mid.block_2.", h)
+    h = _swish(F.group_norm(h, 32, W[e + "norm_out.weight"], W[e + "norm_out.bias"], 1e-6))
+    h = F.conv1d(h, W[e + "conv_out.weight"], W[e + "conv_out.bias"], padding=k // 2)
+    return F.conv1d(h, W["quant_conv.weight"], W["quant_conv.bias"])
+
+
+def mel_spectrogram(y: Tensor, mel_basis: Tensor, n_fft: int = 1024, hop: int = 256, win: int = 1024) -> Tensor:
+    """``MelNet.forward`` (ldm/data/preprocess/NAT_mel.py:66-85, center=False): clamp, reflect pad (n_fft-hop)/2,
+    |STFT| (periodic Hann, onesided, sqrt(re^2 + im^2 + 1e-9)), mel_basis @ mag, log10(clamp(1e-5))."""
+    y = y.clamp(-1.0, 1.0)
+    p = (n_fft - hop) // 2
+    y = F.pad(y.unsqueeze(1), [p, p], mode="reflect").squeeze(1)
+    spec = torch.stft(y, n_fft, hop_length=hop, win_length=win, window=torch.hann_window(win), center=False,
+                      normalized=False, onesided=True, return_complex=True)
+    mag = torch.sqrt(spec.real.pow(2) + spec.imag.pow(2) + 1e-9)
+    return torch.log10(torch.clamp(torch.matmul(mel_basis, mag), min=1e-5))
 
 
 # ---------------------------------------------------------------------------

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import math
 import json
 import os
 import sys
@@ -95,10 +96,10 @@ def save(name, **arrays):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", default="", help="comma-separated fixture groups to (re)generate: base, c2, c4, c5, text "
+    ap.add_argument("--only", default="", help="comma-separated fixture groups to (re)generate: base, c2, c4, c5, text, enc "
                                                "(default: all)")
     args = ap.parse_args()
-    groups = set(filter(None, args.only.split(","))) or {"base", "c2", "c4", "c5", "text"}
+    groups = set(filter(None, args.only.split(","))) or {"base", "c2", "c4", "c5", "text", "enc"}
     if "text" in groups:  # load transformers' model modules before the stubs shadow torchvision
         from transformers import BertConfig, BertModel, T5Config, T5EncoderModel  # noqa: F401
     install_stubs()
@@ -173,6 +174,31 @@ def main():
                 scheduling_lcm.torch.randn = orig
             mel = lcm.decode_first_stage(z)
             save("e2e_S2_prompt31.npz", x_T=xT, noise=noise, latent=z, mel=mel, wav=voc(mel).squeeze(1))
+        if "enc" in groups:
+            # ---- audio -> latent direction: Encoder1D + quant_conv of the reference
+            # AutoencoderKL, and the reference MelNet (NAT_mel.py) with librosa's filterbank restated
+            # (audiolcm_amd/mel.py; librosa is absent, so the filterbank values are parity unpinned)
+            load_exact(lcm.first_stage_model, recipe.vae_encoder_state(0))
+            for M in (624, 40):
+                gx = torch.Generator().manual_seed(400 + M)
+                mel = torch.randn((1, 80, M), generator=gx) * 1.5 - 4.0
+                post = lcm.first_stage_model.encode(mel)
+                save(f"vae_enc_M{M}.npz", mel=mel, moments=post.parameters)
+            from audiolcm_amd.mel import NAT_MEL_16K, mel_filterbank
+            fb = types.ModuleType("librosa.filters")
+            fb.mel = lambda sr, n_fft, n_mels=128, fmin=0.0, fmax=None, **kw: mel_filterbank(sr, n_fft, n_mels, fmin,
+                                                                                            fmax)
+            sys.modules["librosa"] = types.ModuleType("librosa")
+            sys.modules["librosa"].filters = fb
+            sys.modules["librosa.filters"] = fb
+            from ldm.data.preprocess.NAT_mel import MelNet as RefMelNet
+            net = RefMelNet(dict(NAT_MEL_16K))
+            gw = torch.Generator().manual_seed(500)
+            t = torch.arange(256 * 96, dtype=torch.float64) / 16000.0
+            wav = torch.stack([(0.6 * torch.sin(2 * math.pi * 440.0 * t) + 0.3 * torch.sin(2 * math.pi * 3100.0 * t)
+                                ).float() + 0.05 * torch.randn(t.shape, generator=gw),
+                               1.3 * torch.randn(t.shape, generator=gw).clamp(-2, 2)], 0)  # second row clips
+            save("mel_B2.npz", wav=wav, mel_basis=net.mel_basis, mel=net(wav))
         if "c5" in groups:
             # ---- config 5: 30-s long-form vocoder leg (M = 1872 mel frames -> 479,232 samples) ---------
             gm = torch.Generator().manual_seed(300 + 1872)

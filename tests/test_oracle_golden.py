@@ -170,3 +170,38 @@ def test_t5_relative_bucket_matches_product_restatement():
     from audiolcm_amd.text_encoder import relative_position_bucket
     for L in (1, 5, 77, 200):
         assert torch.equal(relative_position_bucket(L), O.t5_relative_bucket(L))
+
+
+def test_vae_encoder_oracle():
+    """Encoder1D + quant_conv (audiolcm.yaml ddconfig) restated vs the reference AutoencoderKL.encode moments."""
+    W = recipe.vae_encoder_state(0)
+    for M in (40, 624):
+        g = golden(f"vae_enc_M{M}.npz")
+        with torch.no_grad():
+            mom = O.vae_encode_moments(W, torch.from_numpy(g["mel"]))
+        assert mom.shape == g["moments"].shape == (1, 40, M // 2)
+        assert rel_l2(mom.numpy(), g["moments"]) < 1e-5
+
+
+def test_mel_front_end_oracle():
+    """NAT_mel.MelNet (reflect pad, |STFT|, mel projection, log10) restated vs the reference run on the restated
+    librosa slaney filterbank (the filterbank itself is parity unpinned: librosa is absent)."""
+    from audiolcm_amd.mel import mel_filterbank
+    g = golden("mel_B2.npz")
+    np.testing.assert_array_equal(mel_filterbank(16000, 1024, 80, 0, 8000), g["mel_basis"])
+    mel = O.mel_spectrogram(torch.from_numpy(g["wav"]), torch.from_numpy(g["mel_basis"]))
+    assert mel.shape == g["mel"].shape == (2, 80, 96)
+    assert rel_l2(mel.numpy(), g["mel"]) < 1e-5
+
+
+def test_mel_filterbank_properties():
+    """Slaney filterbank sanity (the values are unpinned): 80 triangles over 0..8 kHz, non-negative, each filter
+    non-zero on a contiguous band, peaks ordered, area-normalised (sum * bin width ~ 2 / bandwidth scale)."""
+    from audiolcm_amd.mel import mel_filterbank
+    fb = mel_filterbank(16000, 1024, 80, 0, 8000)
+    assert fb.shape == (80, 513) and (fb >= 0).all()
+    peaks = fb.argmax(1)
+    assert (np.diff(peaks) >= 0).all() and peaks[-1] > peaks[0]
+    for row in fb:
+        nz = np.nonzero(row)[0]
+        assert len(nz) > 0 and (np.diff(nz) == 1).all()
