@@ -992,7 +992,7 @@ static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& 
 }
 
 static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& nw, const ConvW& qkvw, const ConvW& ow,
-                    float* h, VaeWs& w);
+                    float* h, float* o_scratch, VaeWs& w);
 
 static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel, int B, int T, void* ws, size_t wsb,
                       hipStream_t s) {
@@ -1019,7 +1019,7 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
   }
   float* h = w.a;
   ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid1, h, w.b, nullptr, h, w));
-  ALCM_TRY(vae_attn(s, split, B, T, C, V.attn_n, V.attn_qkv, V.attn_out, h, w));
+  ALCM_TRY(vae_attn(s, split, B, T, C, V.attn_n, V.attn_qkv, V.attn_out, h, w.c, w));
   ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid2, h, w.b, nullptr, h, w));
   int Tc = T;
   float* spare = w.c;  // third full buffer for channel-changing blocks
@@ -1056,9 +1056,11 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
   return conv(s, split, B, Tc, cl(h, Tc, C), V.conv_out, Out{mel, (int64_t)V.out_ch * Tc, 1, Tc, 1, 0}, o);
 }
 
-// AttnBlock1D (autoencoder1d.py:259-278): single head over T, logit scale C^-1/2; h += proj_out(attn(GN(h)))
+// AttnBlock1D (autoencoder1d.py:259-278): single head over T, logit scale C^-1/2; h += proj_out(attn(GN(h)));
+// o_scratch (B, T, C) holds the attention output and must not alias h
 static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& nw, const ConvW& qkvw, const ConvW& ow,
-                    float* h, VaeWs& w) {
+                    float* h, float* o_scratch, VaeWs& w) {
+  if (o_scratch == h) return set_error(ALCM_E_INVALID, "vae_attn: scratch aliases the activation");
   {
     ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, nw.g, nw.b, w.gsc, w.gsh, s));
     ConvOpts o;
@@ -1086,12 +1088,12 @@ static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& 
     p.b.kind = ALCM_OPND_ACT_T; p.b.ptr = w.qkv + 2 * C; p.b.st = 3 * C; p.b.sc = 1; p.b.T_in = T; p.b.rows = C;
     p.b.zs1 = (int64_t)T * 3 * C;
     p.acc_scale = 1.f; p.out_scale = 1.f;
-    p.out = w.c; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
+    p.out = o_scratch; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
     p.prec = split;
     ALCM_TRY(gemm(p, s));
     ConvOpts oo;
     oo.res = Res{h, (int64_t)T * C, C, 1};
-    ALCM_TRY(conv(s, split, B, T, cl(w.c, T, C), ow, ocl(h, T, C), oo));
+    ALCM_TRY(conv(s, split, B, T, cl(o_scratch, T, C), ow, ocl(h, T, C), oo));
   }
   return 0;
 }
@@ -1138,7 +1140,7 @@ static int vae_encode(alcm_model* m, const float* x, float* moments, int B, int 
     }
   }
   ALCM_TRY(vae_res(s, split, pk, B, T, E.mid1, h, w.b, nullptr, h, w));
-  ALCM_TRY(vae_attn(s, split, B, T, C, E.attn_n, E.attn_qkv, E.attn_out, h, w));
+  ALCM_TRY(vae_attn(s, split, B, T, C, E.attn_n, E.attn_qkv, E.attn_out, h, h == w.c ? w.d : w.c, w));
   ALCM_TRY(vae_res(s, split, pk, B, T, E.mid2, h, w.b, nullptr, h, w));
   ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, E.norm_out.g, E.norm_out.b, w.gsc, w.gsh, s));
   {

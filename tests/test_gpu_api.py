@@ -99,3 +99,23 @@ def test_cli_prompt_txt_and_audiocaps_dataset(gpu, tmp_path):
                      "Y6BJ455B1aAs_sample_0_1.wav", "Y7fmOlUlwoNg_sample_1_0.wav", "Y7fmOlUlwoNg_sample_1_1.wav"]
     assert df["caption"][2].startswith("A rocket flies by")
     assert all(os.path.exists(p) for p in df["audio_path"])
+
+
+def test_vocoder_numpy_vocode_branch(gpu, tmp_path):
+    """VocoderBigVGAN.vocode (vocoder/bigvgan/models.py:406-411) with a numpy (80, M) mel returns a numpy waveform equal
+    to the tensor path; loaded from best_netG.pt + args.yml."""
+    import yaml
+    from audiolcm_amd import recipe
+    from audiolcm_amd.models import VocoderBigVGAN
+    from conftest import golden
+    vd = tmp_path / "voc"
+    vd.mkdir()
+    torch.save({"generator": recipe.bigvgan_state(0)}, str(vd / "best_netG.pt"))
+    (vd / "args.yml").write_text(yaml.safe_dump(BIGVGAN_ARGS))
+    voc = VocoderBigVGAN(str(vd))
+    g = golden("bigvgan_M20.npz")
+    w_np = voc.vocode(g["mel"][0])
+    assert isinstance(w_np, np.ndarray) and w_np.shape == (20 * 256,)
+    w_t = voc.vocode(torch.from_numpy(g["mel"]).cuda()).reshape(-1).cpu().numpy()
+    assert np.array_equal(w_np, w_t)
+    assert np.linalg.norm(w_np - g["wav"].reshape(-1)) / np.linalg.norm(g["wav"]) < 1e-3
