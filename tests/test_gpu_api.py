@@ -48,7 +48,8 @@ def test_checkpoint_ingestion_matches_recipe(gpu, tmp_path):
     for pre in ("model.diffusion_model.", "unet.diffusion_model.", "target_unet.diffusion_model."):
         sd.update({pre + k: v for k, v in dit.items()})
     sd.update({"first_stage_model." + k: v for k, v in recipe.vae_state(0).items()})
-    sd["first_stage_model.encoder.conv_in.weight"] = torch.zeros(384, 80, 5)  # off-path keys are ignored
+    sd.update({"first_stage_model." + k: v for k, v in recipe.vae_encoder_state(0).items()})
+    sd["first_stage_model.loss.discriminator.main.0.weight"] = torch.zeros(64, 1, 4, 4)  # training-only: ignored
     sd.update({"cond_stage_model." + k: v for k, v in recipe.text_state(0).items()})
     sd["scale_factor"] = torch.tensor(1.0)
     sd["alphas_cumprod"] = torch.ones(1000)
