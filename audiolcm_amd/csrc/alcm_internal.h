@@ -77,6 +77,7 @@ struct Knobs {
   bool tail_f16w2_all = false;   // ALCM_TAIL_F16W2_ALL
   bool serial_resblocks = false; // ALCM_SERIAL_RESBLOCKS: default of alcm_model_set_resblock_streams
   bool prof_shapes = false;      // ALCM_PROF_SHAPES: split profile rows per layer shape
+  int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
 };
 const Knobs& knobs();
 

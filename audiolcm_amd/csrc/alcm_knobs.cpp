@@ -33,6 +33,7 @@ static Knobs read_knobs() {
   k.tail_f16w2_all = env_set("ALCM_TAIL_F16W2_ALL");
   k.serial_resblocks = env_set("ALCM_SERIAL_RESBLOCKS");
   k.prof_shapes = env_set("ALCM_PROF_SHAPES");
+  k.tail_prefetch = env_int("ALCM_TAIL_PREFETCH", 1);
   return k;
 }
 

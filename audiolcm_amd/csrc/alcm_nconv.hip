@@ -41,6 +41,7 @@ struct NConvDev {
   int accumulate;
   int tiles_per_batch, tstride, tshift;
   ActEpiDev act;
+  int act_prefetch;  // ACT: residual prefetched into registers before the K loop
 };
 
 constexpr int NC_HALO = 64;  // max (k-1)*dil
@@ -131,6 +132,21 @@ __global__ __launch_bounds__(256) void nconv_kernel(const NConvDev P) {
   // windows + weight step 0 landed; steps 1 .. D-1 stay in flight
   nc_vmcnt<(D - 1) * G>();
 
+  // ACT tiles: residual of every tile row loaded into registers now, consumed by the epilogue
+  constexpr int RPA = ACT ? (BM * (BN / 4) + 255) / 256 : 1;
+  float4 rpa[RPA];
+  const bool prea = ACT && P.res && P.act_prefetch;
+  if (prea) {
+    const int cq = P.N / 4;
+#pragma unroll
+    for (int i = 0; i < RPA; ++i) {
+      const int e = tid + i * 256;
+      const int m = e / cq, n = (e - m * cq) * 4;
+      const int t = min(max(t0 + m, 0), P.T - 1);
+      rpa[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + t) * P.N + (e < BM * cq ? n : 0));
+    }
+  }
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -189,7 +205,27 @@ __global__ __launch_bounds__(256) void nconv_kernel(const NConvDev P) {
   __syncthreads();
   const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
   const int cq = P.N / 4;
-  if (P.res || P.out) {
+  if (prea) {
+#pragma unroll
+    for (int i = 0; i < RPA; ++i) {
+      const int e = tid + i * 256;
+      const int m = e / cq, n = (e - m * cq) * 4;
+      const int t = t0 + m;
+      if (e >= BM * cq || t < 0 || t >= P.T) continue;
+      const int64_t go = ((int64_t)b * P.T + t) * P.N + n;
+      float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+      v.x += rpa[i].x; v.y += rpa[i].y; v.z += rpa[i].z; v.w += rpa[i].w;
+      *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+      if (P.out && t >= e_lo && t < e_hi) {
+        v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+        if (P.accumulate) {
+          const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+          v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+        }
+        *reinterpret_cast<float4*>(P.out + go) = v;
+      }
+    }
+  } else if (P.res || P.out) {
     // (+ res) for every tile row inside [0, T) (the activation reads halo rows); fp32 out for owned rows
     for (int e = tid; e < BM * cq; e += 256) {
       const int m = e / cq, n = (e - m * cq) * 4;
@@ -240,6 +276,7 @@ int nconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   P.w = wplane; P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
+  P.act_prefetch = knobs().tail_prefetch;
   // tile configurations (rows per tile, weight ring depth) sized for >= 2 workgroups per CU where the LDS
   // allows: C = 24 -> 256 x 32, 4 buffers (36 KB, 4 workgroups per CU); C = 48 -> 256 x 64, 4 buffers (72 KB);
   // C = 96 -> 128 x 96, 3 buffers (72 KB)

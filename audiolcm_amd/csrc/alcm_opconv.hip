@@ -164,6 +164,7 @@ struct OpConvDev {
   int tiles_per_batch;
   int tstride, tshift;  // tile i of a batch computes rows [i * tstride - tshift, + BM)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
+  int act_prefetch;     // ACT: residual prefetched into registers before the K loop
 };
 
 constexpr int OC_AW = 48;       // window row stride (elements): conflict-free fragment reads from any start row
@@ -218,6 +219,22 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
 
   // residual prefetch (narrow tiles): tile rows are one contiguous block of mrows * N floats
   float4 rp[RPER];  // dead (and eliminated) unless PRE
+  // ACT tiles: the residual of every tile row (halo rows included) is loaded into registers before the K loop,
+  // so the epilogue does not stall on one dependent global load per float4 (ALCM_TAIL_PREFETCH=0: off, A-B)
+  constexpr int RPA = ACT ? (BM * (BN / 4) + 255) / 256 : 1;
+  float4 rpa[RPA];
+  const bool prea = ACT && P.res && P.act_prefetch;
+  if (prea) {
+    const int cq = P.N / 4;
+#pragma unroll
+    for (int i = 0; i < RPA; ++i) {
+      const int e = tid + i * 256;
+      const int m = e / cq, n = (e - m * cq) * 4;
+      const int t = min(max(t0 + m, 0), P.T - 1);
+      const int64_t go = ((int64_t)b * P.T + t) * P.N + (e < BM * cq ? n : 0);
+      rpa[i] = *reinterpret_cast<const float4*>(P.res + go);
+    }
+  }
   if constexpr (PRE) {
     const int nq = mrows * (P.N / 4);
 #pragma unroll
@@ -408,7 +425,29 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
       }
     __syncthreads();
     const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
-    if (P.res || P.out) {
+    if (prea) {
+      const int cq = P.N / 4;
+#pragma unroll
+      for (int i = 0; i < RPA; ++i) {
+        const int e = tid + i * 256;
+        const int m = e / cq, n = (e - m * cq) * 4;
+        const int t = t0 + m;
+        if (e >= BM * cq || t < 0 || t >= P.T) continue;
+        const int64_t go = ((int64_t)b * P.T + t) * P.N + n;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        v.x += rpa[i].x; v.y += rpa[i].y; v.z += rpa[i].z; v.w += rpa[i].w;
+        *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+        if (P.out && t >= e_lo && t < e_hi) {
+          v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+          if (P.accumulate) {
+            const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+            v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+          }
+          *reinterpret_cast<float4*>(P.out + go) = v;
+        }
+      }
+      __syncthreads();
+    } else if (P.res || P.out) {
       const int cq = P.N / 4;
       for (int e = tid; e < BM * cq; e += 256) {
         const int m = e / cq, n = (e - m * cq) * 4;
@@ -612,6 +651,7 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
+  P.act_prefetch = knobs().tail_prefetch;
   const double M = (double)a.B * a.T;
   const int npa = a.prec == PREC_SPLIT ? 2 : 1, npb = (a.prec == PREC_SPLIT || a.prec == PREC_F16W2) ? 2 : 1;
   const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;

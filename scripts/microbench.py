@@ -208,7 +208,10 @@ def bench_tail(B=32):
             w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
             pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
             line = []
-            for v in os.environ.get("NCONV_VARS", "0,1").split(","):
+            for v in [f"{n}/{pf}" for n in os.environ.get("NCONV_VARS", "0,1").split(",")
+                      for pf in os.environ.get("PF_VARS", "1").split(",")]:
+                v, pf = v.split("/")
+                os.environ["ALCM_TAIL_PREFETCH"] = pf
                 os.environ["ALCM_NCONV"] = v.split(":")[0]
                 _hip.reload_knobs()
                 if ":" in v:
@@ -220,7 +223,7 @@ def bench_tail(B=32):
                 ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
                 ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
                 ms3 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
-                line.append(f"v{v}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
+                line.append(f"v{v}pf{pf}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
             os.environ.pop("ALCM_NCONV")
             _hip.reload_knobs()
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
