@@ -14,6 +14,7 @@
 // element instead of ~30.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
@@ -21,19 +22,22 @@
 
 namespace alcm {
 
-constexpr int AC_TT = 128;                 // output rows per tile
-constexpr int AC_NP = 16;                  // channel pairs per tile (32 channels)
+// Tiles: NP channel pairs x (2048 / NP) output rows.  NP = 32 (64 channels: whole 128-B lines of the fp16
+// output rows and 256-B input row segments) where Cp allows, else NP = 16.
 constexpr int AC_SEG = 18;                 // upsampled samples per phase-1 thread (even: static FIR indexing)
-constexpr int AC_NU = 16 * AC_SEG;         // upsampled samples staged per channel (>= 2 * AC_TT + 11)
-constexpr int AC_RS = AC_NP + 1;           // LDS sample-row stride (f32x2): conflict-free phase-2 row reads
 
-template <int PREC>
+template <int PREC, int AC_NP>
 __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__ x, u16* __restrict__ y,
                                                        int64_t y_lo, int T, int C, int Cp,
                                                        const float* __restrict__ aexp,
                                                        const float* __restrict__ ibeta, const Taps12O f,
                                                        int tiles_t, int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int AC_TT = 2048 / AC_NP;             // output rows per tile (8 per phase-2 thread)
+  constexpr int NSEG = 256 / AC_NP;                // phase-1 segments
+  constexpr int AC_NU = NSEG * AC_SEG;             // upsampled samples staged per channel (>= 2 * AC_TT + 11)
+  constexpr int AC_RS = AC_NP + 1;                 // LDS sample-row stride (f32x2): conflict-free phase-2 reads
+  static_assert(AC_NU >= 2 * AC_TT + 11 && AC_TT == 8 * NSEG, "act_coop tile");
   __shared__ __attribute__((aligned(16))) f32x2 sv[AC_NU * AC_RS];  // [m - m0][pair]
   const int tid = threadIdx.x;
   int bid = blockIdx.x;
@@ -42,7 +46,7 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   const int tt = bid % tiles_t;
   const int b = bid / tiles_t;
   const int t0 = tt * AC_TT, c0 = ct * 2 * AC_NP;
-  const int p = tid & (AC_NP - 1);
+  const int p = tid % AC_NP;
   const int c = c0 + 2 * p;
   const bool live = c < C;  // pairs at or beyond C: operand padding (zeros)
   const float* xb = x + ((int64_t)b * T) * C + (live ? c : 0);
@@ -53,23 +57,27 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   // ---- phase 1: upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
   //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
   if (live) {
-    const int seg = tid >> 4;
+    const int seg = tid / AC_NP;
     const int mb = m0 + seg * AC_SEG;
     const int xlo = mb / 2 - 3;  // sample mb + q reads x rows xlo + (q + 5 - ku) / 2 + 3 - 3
     if (mb >= 0 && mb + AC_SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1) {
       f32x2 win[15];
 #pragma unroll
       for (int i = 0; i < 15; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(xlo + i) * C);
+      // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
+      // order compiles to 6-deep dependent chains with a wait state between links)
+      f32x2 u[AC_SEG];
 #pragma unroll
-      for (int q = 0; q < AC_SEG; ++q) {
-        f32x2 u = f32x2{0.f, 0.f};
+      for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
+      for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+        for (int q = 0; q < AC_SEG; ++q) {
           const int ku = 2 * kk + ((q & 1) ? 0 : 1);
-          u = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u);
+          u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
         }
-        sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
-      }
+#pragma unroll
+      for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
     } else {
       for (int q = 0; q < AC_SEG; ++q) {
         int m = mb + q;
@@ -87,7 +95,7 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   }
   __syncthreads();
   // ---- phase 2: outputs j0 .. j0 + 7 of pair p: o[j] = sum_k dn[k] * sv[2j + k - 5 - m0]
-  const int run = tid >> 4;
+  const int run = tid / AC_NP;
   const int j0 = t0 + run * 8;
   if (j0 >= T) return;
   u16* yb = y + ((int64_t)b * T) * Cp + c;
@@ -100,18 +108,31 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   f32x2 s[26];
 #pragma unroll
   for (int i = 0; i < 26; ++i) s[i] = sp[i * AC_RS];
+  // tap-outer: 8 independent chains (one per output, each summed in ascending tap order like the fused
+  // epilogue's), then the stores (no per-row branch between the chains)
+  f32x2 o[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    f32x2 o = f32x2{0.f, 0.f};
+  for (int r = 0; r < 8; ++r) o[r] = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 12; ++k) o = fma2(f32x2{f.dn[k], f.dn[k]}, s[2 * r + k], o);
-    if (r < jn) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o);
+  for (int k = 0; k < 12; ++k)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, s[2 * r + k], o[r]);
+  if (jn == 8) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
+  } else {
+    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
   }
 }
 
 int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
              const Taps12O& f, int prec, hipStream_t s) {
-  const int tiles_t = (T + AC_TT - 1) / AC_TT, tiles_c = Cp / (2 * AC_NP);
+  // 64-channel tiles (whole 128-B output lines) measured faster at C = 768 (-15 %) and for the two-plane split
+  // output (-10 %), slower at C = 384 (+10..15 %), even at C = 192 fp16 (scripts/microbench.py actnp)
+  const int knp = knobs().act_np;
+  const bool wide = Cp % 64 == 0 && (knp == 32 || (knp == 0 && (C >= 768 || prec == PREC_SPLIT)));
+  const int np = wide ? 32 : 16, tt = 2048 / np;
+  const int tiles_t = (T + tt - 1) / tt, tiles_c = Cp / (2 * np);
   const int64_t nwg = (int64_t)B * tiles_t * tiles_c;
   if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
   const int64_t y_lo = (int64_t)B * T * Cp;
@@ -119,9 +140,14 @@ int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* 
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
                        tiles_t, tiles_c);
   };
-  if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT>);
-  else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16>);
-  else launch(act_coop_kernel<PREC_F16>);
+  auto pick = [&](auto npc) {
+    constexpr int NP = decltype(npc)::value;
+    if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT, NP>);
+    else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16, NP>);
+    else launch(act_coop_kernel<PREC_F16, NP>);
+  };
+  if (wide) pick(std::integral_constant<int, 32>{});
+  else pick(std::integral_constant<int, 16>{});
   return 0;
 }
 

@@ -49,24 +49,41 @@ __device__ __forceinline__ void op_store2(u16* hi, int64_t lo_off, f32x2 v) {
 // Activation1d of R consecutive outputs j0 .. j0+R-1 of a channel pair whose input rows j0-6 .. j0+R+5 are
 // all inside the sequence: win[i] = x[j0 - 6 + i].  Upsampled sample q (m = 2*j0 - 5 + q) feeds outputs r
 // with 0 <= q - 2r <= 11 (down tap k = q - 2r, accumulated in ascending k as DownSample1d's conv does).
-template <int R>
+template <int R, int QB = 4>
 __device__ __forceinline__ void act_run_interior(const f32x2 (&win)[R + 12], const Taps12O& f, f32x2 ear, f32x2 h,
                                                  f32x2 (&o)[R]) {
+  constexpr int NQ = 2 * R + 10;
 #pragma unroll
   for (int r = 0; r < R; ++r) o[r] = f32x2{0.f, 0.f};
+  // QB upsampled samples at a time, tap-outer: QB independent up-filter chains back to back (a q-outer order
+  // compiles to 6-deep dependent chains with a wait state between links); the order of every sum is unchanged
 #pragma unroll
-  for (int q = 0; q < 2 * R + 10; ++q) {
-    f32x2 u = f32x2{0.f, 0.f};
+  for (int q0 = 0; q0 < NQ; q0 += QB) {
+    f32x2 u[QB];
 #pragma unroll
-    for (int kk = 0; kk < 6; ++kk) {
-      const int k = 2 * kk + (q & 1);
-      u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
-    }
-    const f32x2 sv = snake2(u, ear, h);
+    for (int i = 0; i < QB; ++i) u[i] = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int k = q - 2 * r;
-      if (k >= 0 && k < 12) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv, o[r]);
+    for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+      for (int i = 0; i < QB; ++i) {
+        const int q = q0 + i;
+        if (q < NQ) {
+          const int k = 2 * kk + (q & 1);
+          u[i] = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u[i]);
+        }
+      }
+    f32x2 sv[QB];
+#pragma unroll
+    for (int i = 0; i < QB; ++i)
+      if (q0 + i < NQ) sv[i] = snake2(u[i], ear, h);
+#pragma unroll
+    for (int i = 0; i < QB; ++i) {
+      const int q = q0 + i;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = q - 2 * r;
+        if (q < NQ && k >= 0 && k < 12) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv[i], o[r]);
+      }
     }
   }
 }

@@ -62,11 +62,13 @@ int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const voi
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
   int wconv = 8;                 // ALCM_WCONV: 8 = 2-workgroup/CU kernel, 5 = 256-row kernel, 0 = neither
+  int wconv_order = -1;          // ALCM_WCONV_ORDER: wconv2 workgroup order (-1 by shape, 0 M-tile major, 1 N-tile major)
   int wconv_ablate = 0;          // ALCM_WCONV_ABLATE: timing-only ablation bits of the wide-layer kernel
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width
   int nconv_nb = 0;              // ALCM_NCONV_NB: narrow-conv ring depth / tile variant
   int act_rows = 8;              // ALCM_ACT_ROWS: rows per thread of the per-thread Activation1d kernel
   bool act_v1 = false;           // ALCM_ACT_V1: per-thread Activation1d kernel instead of the cooperative one
+  int act_np = 0;                // ALCM_ACT_NP: channel pairs per cooperative Activation1d tile (0 by shape, 16, 32)
   int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
   bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION
   bool wide_act_fusion = false;  // ALCM_WIDE_ACT_FUSION

@@ -19,10 +19,12 @@ static Knobs read_knobs() {
   Knobs k;
   k.wconv = env_int("ALCM_WCONV", 8);
   k.wconv_ablate = env_int("ALCM_WCONV_ABLATE", 0);
+  k.wconv_order = env_int("ALCM_WCONV_ORDER", -1);
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;
   k.act_v1 = env_set("ALCM_ACT_V1");
+  k.act_np = env_int("ALCM_ACT_NP", 0);
   k.opconv_tile = env_int("ALCM_OPCONV_TILE", 0);
   k.no_act_fusion = env_set("ALCM_NO_ACT_FUSION");
   k.wide_act_fusion = env_set("ALCM_WIDE_ACT_FUSION");

@@ -43,6 +43,7 @@ struct WConvDev {
   float out_scale;
   int accumulate;
   int tiles_per_batch, tiles_n, nwg;
+  int n_major;          // workgroup order: 0 = M-tile major (N tiles of an M tile adjacent), 1 = N-tile major
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
 // boundary (the stall is covered by the other workgroup).
 constexpr int W2_BM = 128, W2_BN = 192, W2_WROWS = 192;
 
-template <int PREC, bool GEGLU>
+template <int PREC, bool GEGLU, int AB = 0>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   constexpr int WBUF = W2_WROWS * 128;   // window image (24 KB)
@@ -384,85 +385,117 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = P.nwg >> 3, r8 = P.nwg & 7;
   const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
-  const int mt = wid / P.tiles_n, nt = wid - mt * P.tiles_n;
+  int mt, nt;
+  if (P.n_major) {
+    const int tiles_m = P.nwg / P.tiles_n;
+    nt = wid / tiles_m;
+    mt = wid - nt * tiles_m;
+  } else {
+    mt = wid / P.tiles_n;
+    nt = wid - mt * P.tiles_n;
+  }
   const int b = mt / P.tiles_per_batch;
   const int t0 = (mt - b * P.tiles_per_batch) * W2_BM;
   const int col0 = nt * W2_BN;
   const int K = P.ksize, Cp = P.Cp;
   const int WR = W2_BM + (K - 1) * P.dil;
-  const int nC = Cp / 64;
-  const int steps = nC * K;
-
-  const u16* wsrc[WPW];
-  int wstep[WPW];
-#pragma unroll
-  for (int j = 0; j < WPW; ++j) {
-    const int row = 8 * (wave + 4 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (row & 7);
-    const int ts = t0 - P.pad + row;
-    const bool ok = row < WR && ts >= 0 && ts < P.T;
-    wsrc[j] = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
-    wstep[j] = ok ? 64 : 0;
-  }
-  const u16* bsrc[BPW];
-#pragma unroll
-  for (int j = 0; j < BPW; ++j) {
-    const int n = 8 * (wave + 4 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (n & 7);
-    bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
-  }
-  auto stage_w = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + c * wstep[j], smem + (wave + 4 * j) * 1024);
-  };
-  auto stage_b = [&](int st, int buf) {
-    const int c = st / K, tap = st - c * K;
-    const int off = tap * Cp + c * 64;
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) glds16(bsrc[j] + off, smem + WBUF + buf * BBUF + (wave + 4 * j) * 1024);
-  };
 
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int arow0 = wm * 64 + (lane & 15);
-  const int nrow0 = wn * 96 + (lane & 15);
-  const int bsw = lane & 7;
-
-  stage_w(0);
-  stage_b(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  int st = 0;
-  for (int c = 0; c < nC; ++c) {
-    for (int tap = 0; tap < K; ++tap, ++st) {
-      if (st + 1 < steps) stage_b(st + 1, (st + 1) & 1);
-      const char* Bl = smem + WBUF + (st & 1) * BBUF;
-      const int arow = arow0 + tap * P.dil;
-      const int asw = arow & 7;
+  // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA, 4 no K-loop DMA,
+  // 8 no K-loop waits / barriers
+  constexpr bool no_dma = (AB & 4) != 0, no_mfma = (AB & 2) != 0, no_sync = (AB & 8) != 0;
+  {
+    const int nC = Cp / 64;
+    const int steps = nC * K;
+    const u16* wsrc[WPW];
+    int wstep[WPW];
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        const int ls = 4 * sub + (lane >> 4);
-        bf16x8 af[TM], bfr[TN];
-        const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
-        const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
-      }
-      if (tap == K - 1 && c + 1 < nC) {
-        // every wave has finished reading window c: re-stage it with chunk c + 1
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        stage_w(c + 1);
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int j = 0; j < WPW; ++j) {
+      const int row = 8 * (wave + 4 * j) + (lane >> 3);
+      const int ls = (lane & 7) ^ (row & 7);
+      const int ts = t0 - P.pad + row;
+      const bool ok = row < WR && ts >= 0 && ts < P.T;
+      wsrc[j] = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
+      wstep[j] = ok ? 64 : 0;
     }
+    const u16* bsrc[BPW];
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int n = 8 * (wave + 4 * j) + (lane >> 3);
+      const int ls = (lane & 7) ^ (n & 7);
+      bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
+    }
+    auto stage_w = [&](int c) {
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + c * wstep[j], smem + (wave + 4 * j) * 1024);
+    };
+    auto stage_b = [&](int st, int buf) {
+      const int c = st / K, tap = st - c * K;
+      const int off = tap * Cp + c * 64;
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) glds16(bsrc[j] + off, smem + WBUF + buf * BBUF + (wave + 4 * j) * 1024);
+    };
+
+    const int arow0 = wm * 64 + (lane & 15);
+    const int nrow0 = wn * 96 + (lane & 15);
+    const int bsw = lane & 7;
+
+    stage_w(0);
+    stage_b(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    int st = 0;
+    for (int c = 0; c < nC; ++c) {
+      for (int tap = 0; tap < K; ++tap, ++st) {
+        if (st + 1 < steps && !no_dma) stage_b(st + 1, (st + 1) & 1);
+        const char* Bl = smem + WBUF + (st & 1) * BBUF;
+        const int arow = arow0 + tap * P.dil;
+        const int asw = arow & 7;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          const int ls = 4 * sub + (lane >> 4);
+          bf16x8 af[TM], bfr[TN];
+          const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
+          const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
+          if constexpr (no_mfma) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][1];
+          } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+          }
+        }
+        if constexpr (no_sync) continue;
+        if (tap == K - 1 && c + 1 < nC) {
+          // every wave has finished reading window c: re-stage it with chunk c + 1
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (!no_dma) stage_w(c + 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    }
+    if constexpr (no_sync) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  }
+  if constexpr ((AB & 1) != 0) {
+    float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 123.f) P.out[tid] = sum;
+    return;
   }
 
   // epilogue: one 64-row half of the tile at a time through LDS (the K loop's last barrier retired every
@@ -559,6 +592,13 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     P.w = wplane; P.kpad = a.kpad; P.N = a.N;
     P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
     P.gplane = (u16*)a.geglu_plane;
+    P.ablate = knobs().wconv_ablate;
+    // N-tile-major order where the weight matrix is long (Cp * k >= 4096) and there are enough M tiles to share
+    // an XCD's weight slice: that XCD's N tiles stay in its L2 (C768 k11 -17 %, DiT FFN -3..-10 %); M-major
+    // elsewhere (the N tiles of an M tile share its input window in L2)
+    const int tiles_m = a.B * ((a.T + W2_BM - 1) / W2_BM);
+    const int ord = knobs().wconv_order;
+    P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && tiles_m >= 128);
     P.tiles_per_batch = (a.T + W2_BM - 1) / W2_BM;
     P.tiles_n = a.N / W2_BN;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
@@ -567,7 +607,16 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     void* tok = prof_start(s);
     const dim3 grid((unsigned)nwg2), blk(256);
     const bool gl = a.geglu_plane != nullptr;
-    if (a.prec == PREC_F16) {
+    if (a.prec == PREC_F16 && !gl && P.ablate) {
+      switch (P.ablate) {
+        case 1: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 1>), grid, blk, 0, s, P); break;
+        case 2: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 2>), grid, blk, 0, s, P); break;
+        case 4: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 4>), grid, blk, 0, s, P); break;
+        case 6: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 6>), grid, blk, 0, s, P); break;
+        case 8: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 8>), grid, blk, 0, s, P); break;
+        default: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 3>), grid, blk, 0, s, P); break;
+      }
+    } else if (a.prec == PREC_F16) {
       if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true>), grid, blk, 0, s, P);
       else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false>), grid, blk, 0, s, P);
     } else {

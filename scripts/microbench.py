@@ -30,6 +30,17 @@ def timeit(fn, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
+def spin(seconds=3.0):
+    """hold the GPU busy until its clocks settle: launches timed right after an idle period run up to 15 % slower
+    than the same launches a few seconds later (measured: the first of five identical A/B variants)"""
+    a = torch.randn((8192, 8192), device="cuda", dtype=torch.bfloat16)
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        for _ in range(20):
+            a @ a
+        torch.cuda.synchronize()
+
+
 def bench_conv(B=32):
     cases = [("bigvgan s0 k11d5", 2496, 768, 768, 11, 5), ("bigvgan s1 k7d3", 9984, 384, 384, 7, 3),
              ("bigvgan s2 k3d1", 19968, 192, 192, 3, 1), ("dit ffn0 k9", 467, 576, 4608, 9, 1),
@@ -55,6 +66,27 @@ def bench_act(B=32):
         a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
         ms = timeit(lambda: K.activation1d(x, a, bt, f, f))
         print(f"act1d C={C} T={T}: {ms:.3f} ms {B * T * C * 8 / 1e9 / ms:.2f} TB/s")
+
+
+def bench_actnp(B=32):
+    """cooperative Activation1d -> operand planes: 32-channel vs 64-channel tiles (ALCM_ACT_NP 16 / 32)"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T, p in ((768, 2496, 2), (384, 9984, 2), (192, 19968, 2), (192, 19968, 1)):
+        x = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        npl = 2 if p == 1 else 1
+        gb = B * T * C * (4 + 2 * npl) / 1e9
+        line, outs = [], []
+        for v in os.environ.get("ACT_NP", "16,32").split(","):
+            os.environ["ALCM_ACT_NP"] = v
+            _hip.reload_knobs()
+            ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p), reps=10)
+            outs.append(K.activation1d_op(x, a, bt, f, f, p).clone())
+            line.append(f"np{v} {ms:7.3f} ms {gb / ms:5.2f} TB/s")
+        os.environ.pop("ALCM_ACT_NP")
+        _hip.reload_knobs()
+        same = all(torch.equal(outs[0], o) for o in outs[1:])
+        print(f"act_op C={C:3d} prec={p}: " + " | ".join(line) + f" | identical {same}", flush=True)
 
 
 def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
@@ -146,8 +178,11 @@ def bench_wablate(B=32):
         pl = K.operand_planes(x, 2)
         tf = 2 * B * T * Cin * N * k / 1e12
         line, outs = [], []
-        for wc in os.environ.get("WCONV_VARS", "5").split(","):
+        for wco in [f"{w}/{o}" for w in os.environ.get("WCONV_VARS", "5").split(",")
+                    for o in os.environ.get("ORDERS", "0").split(",")]:
+            wc, order = wco.split("/")
             os.environ["ALCM_WCONV"] = wc
+            os.environ["ALCM_WCONV_ORDER"] = order
             for ab in os.environ.get("ABLATE", "0,1,2,4,6,3").split(","):
                 os.environ["ALCM_WCONV_ABLATE"] = ab
                 _hip.reload_knobs()
@@ -162,14 +197,33 @@ def bench_wablate(B=32):
                     y = fn()
                     yy = y if y is not None else o
                     outs.append((yy.view(torch.float16) if yy.dtype == torch.int16 else yy).float().clone())
-                line.append(f"w{wc}ab{ab} {ms:7.3f}")
+                line.append(f"w{wc}o{order}ab{ab} {ms:7.3f}")
         os.environ.pop("ALCM_WCONV_ABLATE")
+        os.environ.pop("ALCM_WCONV_ORDER")
         os.environ.pop("ALCM_WCONV")
         _hip.reload_knobs()
         ms0 = float(line[0].split()[1])
         diff = max([float((outs[0] - x).abs().max()) for x in outs[1:]] or [0.0])
         print(f"{name:12s} {tf / ms0 * 1e3:7.1f} TF/s | " + " | ".join(line) + f" ms | max|diff| {diff:.2e}",
               flush=True)
+
+
+def bench_wone(B=32):
+    """the WSHAPES wide-layer shapes, 5 launches each with the current ALCM_* settings (target of --pmc passes)"""
+    sel = os.environ.get("WSHAPES", "s0 C768 k11")
+    for name, T, Cin, N, k, d, gl, res, acc in WIDE_SHAPES:
+        if not any(x in name for x in sel.split(",")):
+            continue
+        x = torch.randn((B, T, Cin), device="cuda")
+        w = torch.randn((N, Cin, k), device="cuda") / (Cin * k) ** 0.5
+        r = torch.randn((B, T, N), device="cuda") if res else None
+        o = torch.zeros((B, T, N), device="cuda") if acc else None
+        pw = K.pack_conv_weight(w)
+        pl = K.operand_planes(x, 2)
+        for _ in range(5):
+            K.opconv(pl, Cin, w, None, d, 2, residual=r, packed=pw, accumulate_into=o)
+        torch.cuda.synchronize()
+        print(f"{name}: done", flush=True)
 
 
 def bench_ffn(B=32):
@@ -248,5 +302,6 @@ def bench_op1(B=32):
 if __name__ == "__main__":
     _hip.require_device(0)
     which = sys.argv[1:] or ["op", "conv", "act"]
+    spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"wablate": bench_wablate, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
+        {"wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
