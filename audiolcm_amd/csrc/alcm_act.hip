@@ -151,4 +151,34 @@ int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* 
   return 0;
 }
 
+// fp32 channels-last rows -> MFMA operand planes [rows][Cp] (channels C .. Cp-1 zero), the format `prec` reads:
+// the input of a plane conv whose producer writes fp32 (the BigVGAN upsampler reads the stage output x)
+template <int PREC>
+__global__ void to_planes_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t rows, int C, int Cp,
+                                 int64_t y_lo) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int cq = Cp / 4;
+  if (i >= rows * cq) return;
+  const int64_t r = i / cq;
+  const int c = (int)(i - r * cq) * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < C) v = *reinterpret_cast<const float4*>(x + r * C + c);
+  u16* yp = y + r * Cp + c;
+  op_store2<PREC>(yp, y_lo, f32x2{v.x, v.y});
+  op_store2<PREC>(yp + 2, y_lo, f32x2{v.z, v.w});
+}
+
+int to_planes(const float* x, void* y, int64_t rows, int C, int Cp, int prec, hipStream_t s) {
+  if (!x || !y || rows <= 0 || C <= 0 || C % 4 || Cp % 32 || C > Cp || (((uintptr_t)x) & 15) || (((uintptr_t)y) & 7))
+    return set_error(ALCM_E_INVALID, "to_planes: bad arguments");
+  const int64_t n = rows * (Cp / 4);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  const int64_t lo = rows * Cp;
+  if (prec == PREC_SPLIT) hipLaunchKernelGGL(to_planes_kernel<PREC_SPLIT>, grid, dim3(256), 0, s, x, (u16*)y, rows, C, Cp, lo);
+  else if (prec == PREC_BF16) hipLaunchKernelGGL(to_planes_kernel<PREC_BF16>, grid, dim3(256), 0, s, x, (u16*)y, rows, C, Cp, lo);
+  else hipLaunchKernelGGL(to_planes_kernel<PREC_F16>, grid, dim3(256), 0, s, x, (u16*)y, rows, C, Cp, lo);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace alcm

@@ -21,6 +21,7 @@
 // (new_attention.py:48-55), residual add, output scale, accumulate (BigVGAN mean of
 // resblocks, models.py:193-199), strided store (channels-last or NCT, conv-transpose phases).
 #include <cstdio>
+#include <cstring>
 
 #include "alcm_common.h"
 #include "audiolcm_hip.h"
@@ -644,6 +645,9 @@ static void launch_one(const GemmDev& P, int batch, int ncols, hipStream_t s) {
     char name[128];
     std::snprintf(name, sizeof(name), "alcm::gemm_kernel<%d, %d, %d, %d, %s, %d, %d>", BM, BN, WM, WN,
                   AVEC ? "true" : "false", BKIND, PREC);
+    if (knobs().prof_shapes)  // diagnostics: split the statistics per problem shape
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " M%d N%d K%d x%d", P.M, ncols,
+                    P.Kpad, batch);
     prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
   }
 }
@@ -665,6 +669,9 @@ static void launch_conv(const GemmDev& P, int nbatch, int T_out, hipStream_t s) 
     char name[128];
     std::snprintf(name, sizeof(name), "alcm::conv_kernel<%d, %d, %d, %d, %d, %s>", BM, BN, WM, WN, PREC,
                   PRO ? "true" : "false");
+    if (knobs().prof_shapes)
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d N%d K%d k%d up%d x%d", T_out,
+                    P.N, P.Kpad, P.a.ksize, P.a.up, nbatch);
     prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
   }
 }

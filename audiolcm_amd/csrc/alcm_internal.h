@@ -44,6 +44,8 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
 int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
+// fp32 rows [rows][C] -> operand planes [rows][Cp] in the format of `prec` (SPLIT: lo plane rows * Cp after hi)
+int to_planes(const float* x, void* y, int64_t rows, int C, int Cp, int prec, hipStream_t s);
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
@@ -68,6 +70,7 @@ struct Knobs {
   int nconv_nb = 0;              // ALCM_NCONV_NB: narrow-conv ring depth / tile variant
   int act_rows = 8;              // ALCM_ACT_ROWS: rows per thread of the per-thread Activation1d kernel
   bool act_v1 = false;           // ALCM_ACT_V1: per-thread Activation1d kernel instead of the cooperative one
+  bool ups_fp32 = false;         // ALCM_UPS_FP32: BigVGAN upsamplers on the fp32-operand conv at the base precision
   int act_np = 0;                // ALCM_ACT_NP: channel pairs per cooperative Activation1d tile (0 by shape, 16, 32)
   int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
   bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION

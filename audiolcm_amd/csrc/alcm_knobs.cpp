@@ -25,6 +25,7 @@ static Knobs read_knobs() {
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;
   k.act_v1 = env_set("ALCM_ACT_V1");
   k.act_np = env_int("ALCM_ACT_NP", 0);
+  k.ups_fp32 = env_set("ALCM_UPS_FP32");
   k.opconv_tile = env_int("ALCM_OPCONV_TILE", 0);
   k.no_act_fusion = env_set("ALCM_NO_ACT_FUSION");
   k.wide_act_fusion = env_set("ALCM_WIDE_ACT_FUSION");

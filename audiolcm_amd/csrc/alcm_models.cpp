@@ -1321,8 +1321,27 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const StageW& S = G.st[si];
     const int To = T * S.rate;
     const int pamp = voc_prec(m, (int)si);
-    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188)
+    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188).  Wide stages whose AMP convs
+    // run on single fp16 / bf16 planes (mixed policy: stages 0-2, +1.3e-4 waveform rel-L2 emulated,
+    // scripts/precision_emulate.py 96 tail) take the wide-layer kernel on planes of x with a strided epilogue;
+    // the others the fp32-operand conv at the base precision
+    const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cout % 192 == 0 && S.cin % 64 == 0 &&
+                            S.phase[0].w.cpad == S.cin && !knobs().ups_fp32;
+    if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
     for (int r = 0; r < S.rate; ++r) {
+      if (ups_planes) {
+        const ConvW& cw = S.phase[r];
+        alcm_opconv_args g;
+        std::memset(&g, 0, sizeof(g));
+        g.a = w.pl; g.a_lo_off = (int64_t)B * T * S.cin;
+        g.B = B; g.T = T; g.C = S.cin; g.Cp = S.cin;
+        g.ksize = cw.w.taps; g.dil = 1; g.pad = S.pad[r];
+        g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
+        g.bias = cw.b; g.out = u; g.out_scale = 1.f; g.prec = pamp;
+        g.out_stride = S.rate; g.out_offset = S.off[r]; g.out_rows = To;
+        ALCM_TRY(opconv(g, s));
+        continue;
+      }
       ConvOpts o;
       o.pad = S.pad[r];
       ALCM_TRY(conv(s, split, B, T, cl(x, T, S.cin), S.phase[r],

@@ -616,7 +616,15 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
     return set_error(ALCM_E_INVALID, "opconv: bad arguments");
   if (a.Cp <= 0 || a.Cp % 32) return set_error(ALCM_E_INVALID, "opconv: Cp must be a positive multiple of 32");
   if ((a.ksize - 1) * a.dil > OC_HALO) return set_error(ALCM_E_INVALID, "opconv: receptive field too large");
-  if (2 * a.pad != (a.ksize - 1) * a.dil) return set_error(ALCM_E_INVALID, "opconv: only same-length convs");
+  const bool strided = a.out_stride > 0;
+  if (strided) {
+    if (a.pad < 0 || a.pad > (a.ksize - 1) * a.dil || a.out_offset < 0 || a.out_offset >= a.out_stride ||
+        (int64_t)(a.T - 1) * a.out_stride + a.out_offset >= a.out_rows || !a.out || a.res || a.accumulate ||
+        a.out_act || a.act_plane || a.geglu_plane)
+      return set_error(ALCM_E_INVALID, "opconv: bad strided-output arguments");
+  } else if (2 * a.pad != (a.ksize - 1) * a.dil) {
+    return set_error(ALCM_E_INVALID, "opconv: only same-length convs");
+  }
   if (a.kpad < a.ksize * a.Cp || a.kpad % 32) return set_error(ALCM_E_INVALID, "opconv: kpad mismatch");
   if (a.prec < PREC_BF16 || a.prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "opconv: bad prec");
   if ((((uintptr_t)a.a) & 15) || (((uintptr_t)a.w) & 15) || (a.a_lo_off % 8) || (a.w_lo_off % 8))
@@ -662,6 +670,13 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
     if (!wconv_try(a, P.w, nullptr, flops, bytes, s))
       return set_error(ALCM_E_INVALID, "opconv: GEGLU plane epilogue needs F16/BF16, N % 128 == 0, Cp % 64 == 0, "
                                        "no res/accumulate/act, 4-byte aligned plane");
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
+  if (strided) {  // only the two-workgroup wide-layer kernel has the strided epilogue
+    if (!wconv_try(a, P.w, nullptr, flops, bytes, s))
+      return set_error(ALCM_E_INVALID, "opconv: strided output needs F16/BF16, N % 192 == 0, Cp % 64 == 0, "
+                                       "(k-1)*dil <= 64");
     ALCM_HIP(hipGetLastError());
     return 0;
   }

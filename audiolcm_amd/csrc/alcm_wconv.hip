@@ -44,6 +44,7 @@ struct WConvDev {
   int accumulate;
   int tiles_per_batch, tiles_n, nwg;
   int n_major;          // workgroup order: 0 = M-tile major (N tiles of an M tile adjacent), 1 = N-tile major
+  int ostride, ooff, orows;  // wconv2 output row of input row t: t * ostride + ooff of orows per batch
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
         const int idx = tid + e * 512;
         const int m = idx / cq, n = (idx - m * cq) * 4;
         const int t = min(r0 + m, P.T - 1);
-        const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + col0 + n;
         rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
         pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
         const int idx = tid + e * 512;
         const int m = idx / cq, n = (idx - m * cq) * 4;
         if (r0 + m >= P.T) continue;
-        const int64_t go = ((int64_t)b * P.T + r0 + m) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
         if (P.bias) {
           const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int idx = tid + (e0 + e) * 256;
         const int m = idx / cq, n = (idx - m * cq) * 4;
         const int t = min(r0 + m, P.T - 1);
-        const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + col0 + n;
         rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
         pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int idx = tid + (e0 + e) * 256;
         const int m = idx / cq, n = (idx - m * cq) * 4;
         if (r0 + m >= P.T) continue;
-        const int64_t go = ((int64_t)b * P.T + r0 + m) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
         if (P.bias) {
           const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
@@ -574,24 +575,28 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
 // no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
-  const int var = knobs().wconv;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
+  const int var = knobs().wconv;
+  const bool strided = a.out_stride > 0;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;
-  if (var <= 0 && !act && !a.geglu_plane) return 0;
+  if (var <= 0 && !act && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
   const int BN = a.N % 192 == 0 ? 192 : (a.N % 128 == 0 ? 128 : 0);
   if (!BN) return 0;
-  if (!act && !a.geglu_plane && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
+  if (!act && !a.geglu_plane && !strided && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
-  if (var == 8 && !act && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
+  if ((var == 8 || strided) && !act && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
     P.w = wplane; P.kpad = a.kpad; P.N = a.N;
     P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
     P.gplane = (u16*)a.geglu_plane;
+    P.ostride = strided ? a.out_stride : 1;
+    P.ooff = strided ? a.out_offset : 0;
+    P.orows = strided ? a.out_rows : a.T;
     P.ablate = knobs().wconv_ablate;
     // N-tile-major order where the weight matrix is long (Cp * k >= 4096) and there are enough M tiles to share
     // an XCD's weight slice: that XCD's N tiles stay in its L2 (C768 k11 -17 %, DiT FFN -3..-10 %); M-major
@@ -633,9 +638,11 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     }
     return 1;
   }
+  if (strided) return 0;
   WConvDev P{};
   P.a = (const u16*)a.a;
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
+  P.ostride = 1; P.ooff = 0; P.orows = a.T;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   P.gplane = (u16*)a.geglu_plane;

@@ -345,11 +345,14 @@ def activation1d_op(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
 def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
-           act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False):
+           act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False,
+           strided: Optional[tuple] = None):
     """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
 
     act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
-    planes (NP, B, T, round_up(N, 32)) from the fused epilogue -> (out or None, planes)."""
+    planes (NP, B, T, round_up(N, 32)) from the fused epilogue -> (out or None, planes).
+    strided = (out, stride, offset, pad): one ConvTranspose1d phase, row t -> row t*stride + offset of the
+    fp32 (B, R, N) tensor `out` (written in place and returned), input rows t - pad + tap*dilation."""
     npl, B, T, Cp = planes.shape
     assert planes.dtype == torch.int16 and planes.is_contiguous()
     N, cin, k = w.shape
@@ -362,6 +365,12 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     a.ksize, a.dil, a.pad = k, dilation, (k - 1) * dilation // 2
     a.w, a.w_lo_off, a.kpad, a.N = ptr(packed.data), packed.lo_off, packed.kpad, N
     a.bias = ptr(bias)
+    if strided is not None:
+        out, a.out_stride, a.out_offset, a.pad = strided
+        assert out.is_contiguous() and out.shape[0] == B and out.shape[2] == N
+        a.out, a.out_rows, a.out_scale, a.prec = ptr(out), out.shape[1], 1.0, int(prec)
+        check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
+        return out
     a.res = ptr(residual.contiguous()) if residual is not None else None
     if accumulate_into is not None:
         out = accumulate_into

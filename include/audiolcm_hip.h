@@ -193,6 +193,12 @@ typedef struct alcm_opconv_args {
    * as an operand plane [B][T][N/2] in the format of `prec` (F16 / BF16) instead of the fp32 output; needs
    * res == NULL, out_act == 0 and the wide-layer kernel (N % 128 == 0, Cp % 64 == 0). */
   void* geglu_plane;
+  /* optional strided output (one phase of a ConvTranspose1d, vocoder/bigvgan/models.py:160-165): when
+   * out_stride > 0, output row t of batch b is row t * out_stride + out_offset of an fp32 [B][out_rows][N]
+   * `out`, and `pad` may be any value in [0, (ksize-1)*dil] (input row t - pad + tap*dil, zero outside).
+   * Needs F16/BF16, N % 192 == 0, Cp % 64 == 0 and no res / accumulate / out_act / act / GEGLU.
+   * 0 (the zero-initialised default): same-length conv, out is [B][T][N]. */
+  int out_stride, out_offset, out_rows;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 

@@ -54,8 +54,9 @@ def run(W, mel, policy, wscale=False):
         return real_conv(x, w, b, stride, padding, dilation, groups)
 
     def convt(x, w, b=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
-        if groups == 1:
-            x, w = q(x, w, "ups")
+        if groups == 1:  # per-stage groups ups0 .. ups5 fall back to "ups"
+            i = state["ups"] = state.get("ups", -1) + 1
+            x, w = q(x, w, f"ups{i}" if f"ups{i}" in policy else "ups")
         return real_convt(x, w, b, stride, padding, output_padding, groups, dilation)
 
     ns = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("_")})
@@ -110,6 +111,10 @@ def main():
             cases["mixed(s3 F16) + ups F16"] = dict(base2, ups=("f16", "f16"))
             cases["mixed(s3 F16) + pre F16W2"] = dict(base2, pre=("f16", "f32"))
             cases["mixed(s3 F16) + ups bf16"] = dict(base2, ups=("bf16", "bf16"))
+            wide_ups = {f"ups{i}": ("f16", "f16") for i in range(3)}
+            cases["mixed(s3 F16) + ups0-2 F16"] = dict(base2, **wide_ups)
+            cases["mixed(s3 F16) + ups0-2 F16, ups3-5 F16W2"] = dict(base2, ups=("f16", "f32"), **wide_ups)
+            cases["mixed(s3 F16) + ups0-3 F16"] = dict(base2, ups3=("f16", "f16"), **wide_ups)
         for name, pol in cases.items():
             for ws in ((False, True) if any(v[1] == "f16" for v in pol.values()) else (False,)):
                 out = run(W, mel, pol, wscale=ws)

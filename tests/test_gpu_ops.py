@@ -332,6 +332,30 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
         assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2)])
+def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
+    """ConvTranspose1d(Cin, N, 2*rate, rate, padding=rate/2) (BigVGAN upsampler, models.py:160-165) as `rate`
+    phase convs on operand planes with the strided epilogue (wide-layer kernel), vs torch's fp32
+    conv_transpose1d on the same plane-rounded input and weight."""
+    B, k = 2, 2 * rate
+    x = _r((B, T, Cin), 30)
+    w, bias = _r((Cin, N, k), 31, 1.0 / np.sqrt(Cin * 2)), _r((N,), 32, 0.05)
+    pl = K.operand_planes(dev(x), prec)
+    rd = (lambda t: t.half().float()) if prec == 2 else (lambda t: t.bfloat16().float())
+    ref = torch.nn.functional.conv_transpose1d(rd(x).transpose(1, 2), rd(w), bias, stride=rate, padding=rate // 2)
+    out = dev(torch.full((B, T * rate, N), float("nan")))
+    pad, Q = rate // 2, 2
+    shape_only = dev(torch.zeros((N, Cin, Q)))
+    for r in range(rate):  # phase r writes outputs t = rate*v + o from inputs v - pad_r .. v - pad_r + Q - 1
+        o = (r - pad) % rate
+        c = (o + pad - r) // rate
+        pw = K.pack_conv_weight(dev(w), transposed=True, stride=rate, phase=r)
+        K.opconv(pl, Cin, shape_only, dev(bias), 1, prec, packed=pw, strided=(out, rate, o, Q - 1 - c))
+    got = out.cpu().transpose(1, 2).numpy()
+    assert np.isfinite(got).all()
+    assert rel_l2(got, ref.numpy()) < 2e-6
+
+
 @pytest.mark.parametrize("C,T,k,dil,prec", [(24, 1000, 11, 5, 3), (48, 700, 7, 3, 3), (96, 500, 3, 1, 3),
                                             (96, 333, 11, 5, 1), (24, 250, 3, 1, 2), (48, 37, 7, 1, 0),
                                             (768, 600, 11, 5, 2), (384, 1100, 7, 3, 2), (192, 1500, 3, 1, 0),
