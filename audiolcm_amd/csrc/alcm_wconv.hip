@@ -409,6 +409,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA, 4 no K-loop DMA,
   // 8 no K-loop waits / barriers
   constexpr bool no_dma = (AB & 4) != 0, no_mfma = (AB & 2) != 0, no_sync = (AB & 8) != 0;
+  constexpr bool no_win = (AB & 16) != 0, no_wdma = (AB & 32) != 0;  // 16: no window re-stage, 32: no weight DMA
   {
     const int nC = Cp / 64;
     const int steps = nC * K;
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     int st = 0;
     for (int c = 0; c < nC; ++c) {
       for (int tap = 0; tap < K; ++tap, ++st) {
-        if (st + 1 < steps && !no_dma) stage_b(st + 1, (st + 1) & 1);
+        if (st + 1 < steps && !no_dma && !no_wdma) stage_b(st + 1, (st + 1) & 1);
         const char* Bl = smem + WBUF + (st & 1) * BBUF;
         const int arow = arow0 + tap * P.dil;
         const int asw = arow & 7;
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
           }
         }
         if constexpr (no_sync) continue;
-        if (tap == K - 1 && c + 1 < nC) {
+        if (tap == K - 1 && c + 1 < nC && !no_win) {
           // every wave has finished reading window c: re-stage it with chunk c + 1
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
           if (!no_dma) stage_w(c + 1);
@@ -619,6 +620,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
         case 4: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 4>), grid, blk, 0, s, P); break;
         case 6: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 6>), grid, blk, 0, s, P); break;
         case 8: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 8>), grid, blk, 0, s, P); break;
+        case 16: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 16>), grid, blk, 0, s, P); break;
+        case 17: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 17>), grid, blk, 0, s, P); break;
+        case 32: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 32>), grid, blk, 0, s, P); break;
         default: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 3>), grid, blk, 0, s, P); break;
       }
     } else if (a.prec == PREC_F16) {
