@@ -132,17 +132,21 @@ __device__ __forceinline__ void act_epilogue_tile(const float* tile, int ots, in
                                                   int nthr) {
   constexpr float INV_PI = 0.318309886183790671538f;
   const int npairs = ncol >> 1;
+  const int nreal = max(0, min(npairs, (C - c0) >> 1));  // pairs with channels < C (C even)
   const int nrun = (e_hi - e_lo + R - 1) / R;
-  for (int w = tid; w < npairs * nrun; w += nthr) {
-    const int run = w / npairs, p = w - run * npairs;
+  // operand padding (channels >= C): zeros, one (row, pair) per item
+  const int npad = npairs - nreal;
+  for (int w = tid; w < npad * (e_hi - e_lo); w += nthr) {
+    const int row = w / npad, p = nreal + (w - row * npad);
+    op_store2<PREC>(A.plane + ((int64_t)b * T + e_lo + row) * A.Cp + c0 + 2 * p, A.plane_lo, f32x2{0.f, 0.f});
+  }
+  // real pairs: every lane of a wave computes (no padding lanes inside the Activation1d work)
+  for (int w = tid; w < nreal * nrun; w += nthr) {
+    const int run = w / nreal, p = w - run * nreal;
     const int c = c0 + 2 * p;
     const int j0 = e_lo + run * R;
     const int jn = min(R, e_hi - j0);
     u16* yb = A.plane + ((int64_t)b * T) * A.Cp + c;
-    if (c >= C) {
-      for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, f32x2{0.f, 0.f});
-      continue;
-    }
     const float* col = tile + 2 * p;
     const f32x2 ear = f32x2{A.aexp[c], A.aexp[c + 1]} * INV_PI;
     const f32x2 h = f32x2{A.ibeta[c], A.ibeta[c + 1]} * 0.5f;
