@@ -1321,11 +1321,13 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const StageW& S = G.st[si];
     const int To = T * S.rate;
     const int pamp = voc_prec(m, (int)si);
-    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188).  Wide stages whose AMP convs
-    // run on single fp16 / bf16 planes (mixed policy: stages 0-2, +1.3e-4 waveform rel-L2 emulated,
-    // scripts/precision_emulate.py 96 tail) take the wide-layer kernel on planes of x with a strided epilogue;
-    // the others the fp32-operand conv at the base precision
-    const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cout % 192 == 0 && S.cin % 64 == 0 &&
+    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188).  Stages whose AMP convs run
+    // on single fp16 / bf16 planes (mixed policy: stages 0-3, +1.9e-4 waveform rel-L2 emulated,
+    // scripts/precision_emulate.py 96 tail) take a plane conv of x with a strided epilogue (the wide-layer
+    // kernel for N % 192 == 0, opconv_kernel for N <= 96); the others the fp32-operand conv at the base
+    // precision
+    const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cin % 32 == 0 &&
+                            (S.cout % 192 == 0 || (S.cout <= 96 && S.cout % 4 == 0)) &&
                             S.phase[0].w.cpad == S.cin && !knobs().ups_fp32;
     if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
     for (int r = 0; r < S.rate; ++r) {

@@ -165,6 +165,7 @@ struct OpConvDev {
   int tstride, tshift;  // tile i of a batch computes rows [i * tstride - tshift, + BM)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
   int act_prefetch;     // ACT: residual prefetched into registers before the K loop
+  int ostride, ooff, orows;  // output row of conv row t: b * orows + t * ostride + ooff (a ConvTranspose phase)
 };
 
 constexpr int OC_AW = 48;       // window row stride (elements): conflict-free fragment reads from any start row
@@ -502,7 +503,7 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
       const int nq = rows * cq;
       for (int e = tid; e < (rows > 0 ? nq : 0); e += 256) {
         const int m = e / cq, n = (e - m * cq) * 4;
-        const int64_t go = (rowbase + r0 + m) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)(t0 + r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
         float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (PRE && P.N <= BN) {
@@ -660,6 +661,9 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
   P.act_prefetch = knobs().tail_prefetch;
+  P.ostride = strided ? a.out_stride : 1;
+  P.ooff = strided ? a.out_offset : 0;
+  P.orows = strided ? a.out_rows : a.T;
   const double M = (double)a.B * a.T;
   const int npa = a.prec == PREC_SPLIT ? 2 : 1, npb = (a.prec == PREC_SPLIT || a.prec == PREC_F16W2) ? 2 : 1;
   const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;
@@ -673,14 +677,15 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
     ALCM_HIP(hipGetLastError());
     return 0;
   }
-  if (strided) {  // only the two-workgroup wide-layer kernel has the strided epilogue
-    if (!wconv_try(a, P.w, nullptr, flops, bytes, s))
-      return set_error(ALCM_E_INVALID, "opconv: strided output needs F16/BF16, N % 192 == 0, Cp % 64 == 0, "
-                                       "(k-1)*dil <= 64");
-    ALCM_HIP(hipGetLastError());
-    return 0;
-  }
-  if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s) ||
+  if (strided) {  // the two-workgroup wide-layer kernel, or opconv_kernel's LDS-staged epilogue (N <= 96)
+    if (wconv_try(a, P.w, nullptr, flops, bytes, s)) {
+      ALCM_HIP(hipGetLastError());
+      return 0;
+    }
+    if (a.N % 4 || a.N > 96)
+      return set_error(ALCM_E_INVALID, "opconv: strided output needs the wide-layer kernel (F16/BF16, N % 192 == 0, "
+                                       "Cp % 64 == 0, (k-1)*dil <= 64) or N <= 96 with N % 4 == 0");
+  } else if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s) ||
       nconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s)) {
     ALCM_HIP(hipGetLastError());
     return 0;

@@ -332,10 +332,11 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
         assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2)])
+@pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
+                                                 (192, 96, 900, 2, 2), (96, 48, 333, 2, 0)])
 def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
     """ConvTranspose1d(Cin, N, 2*rate, rate, padding=rate/2) (BigVGAN upsampler, models.py:160-165) as `rate`
-    phase convs on operand planes with the strided epilogue (wide-layer kernel), vs torch's fp32
+    phase convs on operand planes with the strided epilogue (wide-layer kernel; opconv_kernel for N <= 96), vs torch's fp32
     conv_transpose1d on the same plane-rounded input and weight."""
     B, k = 2, 2 * rate
     x = _r((B, T, Cin), 30)
