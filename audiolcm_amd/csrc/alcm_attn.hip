@@ -44,8 +44,13 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict
   __shared__ __attribute__((aligned(16))) u16 Vt[FA_DV * FA_VS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, cq = lane & 15;
-  const int z = blockIdx.y, b = z / nh, h = z - b * nh;
-  const int q0 = blockIdx.x * FA_Q + wave * 16;
+  // XCD-aware order (1-D grid of nqt * B * nh workgroups, dispatched round-robin over the 8 XCDs): each XCD takes a
+  // contiguous block of work ids, so the query tiles of one (b, head) share that XCD's L2 copy of its K / V
+  const int nwg = (int)gridDim.x, nqt = (L + FA_Q - 1) / FA_Q;
+  const int orig = blockIdx.x, xcd = orig & 7, qx = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (qx + 1) : r8 * (qx + 1) + (xcd - r8) * qx) + (orig >> 3);
+  const int z = wid / nqt, b = z / nh, h = z - b * nh;
+  const int q0 = (wid - z * nqt) * FA_Q + wave * 16;
   const int64_t rs = 3 * (int64_t)H;  // qkv row stride
   const float* base = qkv + (int64_t)b * L * rs + h * dh;
 
@@ -179,6 +184,177 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(const float* __restrict
     }
 }
 
+
+// Resident-K/V form (L <= FR_MAXL): one workgroup of 16 waves per (b, head) stages the head's whole K and V^T
+// once (fp32 -> operand format, 157 KB of LDS at L = 512) and every wave then walks its 16-query blocks over
+// all key tiles with no further barrier.  The tiled kernel above re-reads K/V from HBM once per 64-query
+// workgroup (8x at L = 467); here each head's K/V leave HBM once, and B * heads workgroups (256 at B = 32)
+// fill the 256 CUs one per CU.  Same arithmetic and rounding as the tiled kernel (identical per-tile sums).
+constexpr int FR_MAXL = 512;   // keys padded to a multiple of 64
+constexpr int FR_KS = 80;      // K row stride (elements, 160 B): conflict-free ds_read_b128; dims dh..79 zero
+constexpr int FR_MAXDH = 72;
+constexpr int FR_THREADS = 1024;  // 16 waves: 4 per SIMD hide the per-tile softmax / LDS latency chain
+
+template <int PREC>
+__global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float* __restrict__ qkv, float* __restrict__ O,
+                                                             u16* __restrict__ Op, int L, int Lp, int H, int nh,
+                                                             int dh, float scale) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[FR_MAXL * FR_KS];
+  __shared__ __attribute__((aligned(16))) u16 Vt[FR_MAXDH * (FR_MAXL + 8)];
+  const int VS = Lp + 8;  // V^T row stride: (VS * 2 / 4) mod 64 = 4 * odd -> conflict-free ds_read_b64
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, cq = lane & 15;
+  const int z = blockIdx.x, b = z / nh, h = z - b * nh;
+  const int64_t rs = 3 * (int64_t)H;
+  const float* base = qkv + (int64_t)b * L * rs + h * dh;
+
+  // stage K [key][dim] (dims >= dh and keys >= L zero) and V^T [dim][key] (keys >= L zero); 8 items per thread
+  // per round so 16 float4 loads are in flight per lane (the staging phase is HBM-latency bound otherwise)
+  constexpr int FU = 5;
+  const int nitem = Lp * (FR_KS / 4);
+  for (int e0 = tid; e0 < nitem; e0 += FR_THREADS * FU) {
+    float4 kv[FU], vv[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const int e = e0 + FR_THREADS * u;
+      const int kr = e / (FR_KS / 4), d4 = (e - kr * (FR_KS / 4)) * 4;
+      kv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nitem && kr < L && d4 < dh) {
+        const float* r = base + (int64_t)kr * rs + d4;
+        kv[u] = *reinterpret_cast<const float4*>(r + H);
+        vv[u] = *reinterpret_cast<const float4*>(r + 2 * H);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const int e = e0 + FR_THREADS * u;
+      if (e >= nitem) break;
+      const int kr = e / (FR_KS / 4), d4 = (e - kr * (FR_KS / 4)) * 4;
+      uint2 kp;
+      kp.x = (uint32_t)fa_cvt<PREC>(kv[u].x) | ((uint32_t)fa_cvt<PREC>(kv[u].y) << 16);
+      kp.y = (uint32_t)fa_cvt<PREC>(kv[u].z) | ((uint32_t)fa_cvt<PREC>(kv[u].w) << 16);
+      *reinterpret_cast<uint2*>(&Ks[kr * FR_KS + d4]) = kp;
+      if (d4 < dh) {
+        Vt[(d4 + 0) * VS + kr] = fa_cvt<PREC>(vv[u].x);
+        Vt[(d4 + 1) * VS + kr] = fa_cvt<PREC>(vv[u].y);
+        Vt[(d4 + 2) * VS + kr] = fa_cvt<PREC>(vv[u].z);
+        Vt[(d4 + 3) * VS + kr] = fa_cvt<PREC>(vv[u].w);
+      }
+    }
+  }
+  __syncthreads();
+
+  const int nqb = (L + 15) / 16, nkt = Lp / FA_KT;
+  for (int qb = wave; qb < nqb; qb += FR_THREADS / 64) {
+    const int q0 = qb * 16;
+    bf16x8 qf[3];
+    {
+      const int q = q0 + cq;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        u16 e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int d = 32 * ks + 8 * g + j;
+          e[j] = fa_cvt<PREC>((q < L && d < dh) ? base[(int64_t)q * rs + d] : 0.f);
+        }
+        qf[ks] = __builtin_bit_cast(bf16x8, e);
+      }
+    }
+    f32x4 o[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int k0 = kt * FA_KT;
+      f32x4 s[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          // dims 32 ks + 8 g .. + 7 beyond the 80-element row are zero (only ks = 2, g >= 2)
+          bf16x8 kf = bf16x8{};
+          if (ks < 2 || g < 2) kf = *reinterpret_cast<const bf16x8*>(&Ks[(k0 + 16 * kb + cq) * FR_KS + 32 * ks + 8 * g]);
+          s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * kb + 4 * g + r;
+          const float v = key < L ? s[kb][r] * scale : -INFINITY;
+          s[kb][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mn = fmaxf(m, tmax);
+      const float alpha = __expf(m - mn);
+      m = mn;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __expf(s[kb][r] - mn);
+          s[kb][r] = pv;
+          psum += pv;
+        }
+      l = l * alpha + psum;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        u16 pe[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pe[r] = fa_cvt<PREC>(s[2 * ks][r]);
+          pe[4 + r] = fa_cvt<PREC>(s[2 * ks + 1][r]);
+        }
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, pe);
+#pragma unroll
+        for (int db = 0; db < 5; ++db) {
+          uint4 vv = make_uint4(0u, 0u, 0u, 0u);  // V^T rows >= dh are zero
+          if (16 * db + cq < dh) {
+            const u16* vr = &Vt[(16 * db + cq) * VS + k0 + 32 * ks + 4 * g];
+            const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+            const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+            vv = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          }
+          o[db] = mfma16<PREC>(__builtin_bit_cast(bf16x8, vv), pf, o[db]);
+        }
+      }
+    }
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    const int q = q0 + cq;
+    if (q >= L) continue;
+    const float inv = 1.0f / l;
+    const int64_t ob = ((int64_t)b * L + q) * H + h * dh;
+    if (Op) {
+#pragma unroll
+      for (int db = 0; db < 5; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = 16 * db + 4 * g + r;
+          if (d < dh) Op[ob + d] = fa_cvt<PREC>(o[db][r] * inv);
+        }
+    } else {
+#pragma unroll
+      for (int db = 0; db < 5; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = 16 * db + 4 * g + r;
+          if (d < dh) O[ob + d] = o[db][r] * inv;
+        }
+    }
+  }
+}
+
 // qkv: (B, L, 3H) fp32 rows [q | k | v], head h at columns h*dh; O: (B, L, H) fp32
 int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s, void* o_plane) {
   if (!qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
@@ -186,8 +362,29 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
   if (dh > 72 || dh % 4 || H % 4) return set_error(ALCM_E_INVALID, "flash_attention: head dim must be <= 72, % 4");
   if (prec != PREC_F16 && prec != PREC_BF16) return set_error(ALCM_E_INVALID, "flash_attention: F16 or BF16 only");
   if (((uintptr_t)qkv) & 15) return set_error(ALCM_E_INVALID, "flash_attention: qkv must be 16-byte aligned");
-  const dim3 grid((L + FA_Q - 1) / FA_Q, B * nh);
   const float scale = 1.0f / std::sqrt((float)dh);
+  const int Lp = (L + FA_KT - 1) / FA_KT * FA_KT;
+  if (Lp <= FR_MAXL && dh <= FR_MAXDH && !knobs().attn_tiled && (int64_t)B * nh < (1ll << 31)) {
+    void* tok = prof_start(s);
+    const dim3 grid((unsigned)(B * nh));
+    if (prec == PREC_F16)
+      hipLaunchKernelGGL(flash_attn_res_kernel<PREC_F16>, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh, dh,
+                         scale);
+    else
+      hipLaunchKernelGGL(flash_attn_res_kernel<PREC_BF16>, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh,
+                         dh, scale);
+    if (tok) {
+      char name[64];
+      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d>", prec);
+      const double z = (double)B * nh;
+      prof_stop(tok, s, name, z * 4.0 * L * (double)L * dh, (double)B * L * (3.0 * H + H) * 4.0);
+    }
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
+  const int64_t nwg = (int64_t)((L + FA_Q - 1) / FA_Q) * B * nh;
+  if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "flash_attention: problem too large");
+  const dim3 grid((unsigned)nwg);
   void* tok = prof_start(s);
   if (prec == PREC_F16)
     hipLaunchKernelGGL(flash_attn_kernel<PREC_F16>, grid, dim3(256), 0, s, qkv, O, (u16*)o_plane, L, H, nh, dh, scale);

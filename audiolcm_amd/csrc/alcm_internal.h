@@ -76,6 +76,7 @@ struct Knobs {
   bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION
   bool wide_act_fusion = false;  // ALCM_WIDE_ACT_FUSION
   bool no_flash = false;         // ALCM_NO_FLASH
+  bool attn_tiled = false;       // ALCM_ATTN_TILED: 64-query tiled flash kernel even where K/V fit in LDS
   bool no_attn_planes = false;   // ALCM_NO_ATTN_PLANES
   bool no_ffn_planes = false;    // ALCM_NO_FFN_PLANES
   bool no_vae_planes = false;    // ALCM_NO_VAE_PLANES

@@ -30,6 +30,7 @@ static Knobs read_knobs() {
   k.no_act_fusion = env_set("ALCM_NO_ACT_FUSION");
   k.wide_act_fusion = env_set("ALCM_WIDE_ACT_FUSION");
   k.no_flash = env_set("ALCM_NO_FLASH");
+  k.attn_tiled = env_set("ALCM_ATTN_TILED");
   k.no_attn_planes = env_set("ALCM_NO_ATTN_PLANES");
   k.no_ffn_planes = env_set("ALCM_NO_FFN_PLANES");
   k.no_vae_planes = env_set("ALCM_NO_VAE_PLANES");

@@ -283,6 +283,26 @@ def bench_tail(B=32):
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
 
 
+def bench_act1(B=32):
+    """one standalone Activation1d launch (C = 384 stage-1 shape, fp16 planes) and one fused tail conv (C = 96 k11,
+    residual + Activation1d epilogue), 3 launches each (target of rocprofv3 --pmc passes)"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    x = torch.randn((B, 9984, 384), device="cuda")
+    a, bt = torch.randn(384, device="cuda") * 0.3, torch.randn(384, device="cuda") * 0.3
+    for _ in range(3):
+        K.activation1d_op(x, a, bt, f, f, 2)
+    C, T = 96, 39936
+    x = torch.randn((B, T, C), device="cuda")
+    r = torch.randn((B, T, C), device="cuda")
+    a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+    pl = K.operand_planes(x, 2)
+    w = torch.randn((C, C, 11), device="cuda") * (0.5 / (C * 11) ** 0.5)
+    pw = K.pack_conv_weight(w)
+    for _ in range(3):
+        K.opconv(pl, C, w, None, 5, 2, residual=r, packed=pw, act=(a, bt, f, f))
+    torch.cuda.synchronize()
+
+
 def bench_op1(B=32):
     """one act_op + one opconv launch per tail/wide shape (target of rocprofv3 --pmc passes)"""
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
@@ -304,4 +324,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

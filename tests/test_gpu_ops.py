@@ -138,10 +138,12 @@ def test_attention_products(K, Z, L, d):
     assert rel_l2(o.numpy(), torch.einsum("bij,bjd->bid", p, v).numpy()) < SPLIT_TOL
 
 
-@pytest.mark.parametrize("B,L,heads,dh", [(2, 467, 8, 72), (1, 40, 8, 72), (3, 130, 4, 64), (1, 1, 2, 36)])
+@pytest.mark.parametrize("B,L,heads,dh", [(2, 467, 8, 72), (1, 40, 8, 72), (3, 130, 4, 64), (1, 1, 2, 36), (2, 512, 8, 72),
+                                          (1, 700, 8, 72)])
 @pytest.mark.parametrize("prec", [2, 0])
 def test_flash_attention(K, B, L, heads, dh, prec):
-    """Fused attention (online softmax, scores on chip) vs fp32 softmax(q k^T / sqrt(dh)) v."""
+    """Fused attention (online softmax, scores on chip) vs fp32 softmax(q k^T / sqrt(dh)) v: the resident-K/V kernel
+    (L <= 512) and the 64-query tiled kernel (L = 700)."""
     H = heads * dh
     qkv = _r((B, L, 3 * H), 100, 1.5)
     q, k, v = qkv.split(H, dim=-1)
