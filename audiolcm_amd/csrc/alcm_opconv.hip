@@ -177,8 +177,10 @@ __device__ __forceinline__ int oc_boff(int r, int kq) { return r * 32 + ((kq ^ (
 // over the dead window/weight buffers, RG row groups (of TM*16 rows) at a time, and written as whole
 // BN-column row segments with 16-byte stores (residual read the same way).  VEC = N % 4 == 0.
 // PRE: prefetch the residual into registers at kernel start (narrow tiles whose tile fits one round).
-template <int BM, int BN, int WGM, int WGN, int PREC, int TPS, bool VEC, bool ACT>
-__global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
+// ACT3: fused-activation tiles without a residual (the dilated conv1 of an AMPBlock layer) built for 3 workgroups
+// per CU (<= 168 registers); with a residual the 2-workgroup build keeps its register prefetch of the residual rows
+template <int BM, int BN, int WGM, int WGN, int PREC, int TPS, bool VEC, bool ACT, bool ACT3 = false>
+__global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvDev P) {
   constexpr int TM = BM / (WGM * 16);
   constexpr int TN = BN / (WGN * 16);
   constexpr int NPA = PREC == PREC_SPLIT ? 2 : 1;
@@ -222,9 +224,11 @@ __global__ __launch_bounds__(256) void opconv_kernel(const OpConvDev P) {
   float4 rp[RPER];  // dead (and eliminated) unless PRE
   // ACT tiles: the residual of every tile row (halo rows included) is loaded into registers before the K loop,
   // so the epilogue does not stall on one dependent global load per float4 (ALCM_TAIL_PREFETCH=0: off, A-B)
-  constexpr int RPA = ACT ? (BM * (BN / 4) + 255) / 256 : 1;
+  // (not in the ACT3 build: the 48 registers would spill)
+  constexpr bool PREA_OK = ACT && !ACT3;
+  constexpr int RPA = PREA_OK ? (BM * (BN / 4) + 255) / 256 : 1;
   float4 rpa[RPA];
-  const bool prea = ACT && P.res && P.act_prefetch;
+  const bool prea = PREA_OK && P.res && P.act_prefetch;
   if (prea) {
     const int cq = P.N / 4;
 #pragma unroll
@@ -556,6 +560,14 @@ template <int BM, int BN, int WGM, int WGN, int TPS, bool VEC, bool ACT>
 static void launch_opconv_v(const OpConvDev& Q, dim3 grid, int prec, hipStream_t s) {
   constexpr int TPS_SPLIT = BN >= 192 ? 1 : TPS;  // LDS: the split operands double both buffers
   constexpr bool SPLIT_FITS = 2 * 2 * (BM + OC_HALO) * OC_AW * 2 + 2 * 2 * TPS_SPLIT * BN * 32 * 2 <= 160 * 1024;
+  if constexpr (ACT && BM == 128) {
+    // conv1 (no residual) of C = 96 at fp16: the 3-workgroup build (-11..-13 % per launch, scripts/microbench.py
+    // tail; the same 128-row build for C = 48 measured +10 % at k11 against its 256-row tiles and is not used)
+    if (!Q.res && prec == PREC_F16) {
+      hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_F16, TPS, VEC, ACT, true>), grid, dim3(256), 0, s, Q);
+      return;
+    }
+  }
   if (prec == PREC_SPLIT) {
     if constexpr (SPLIT_FITS)
       hipLaunchKernelGGL((opconv_kernel<BM, BN, WGM, WGN, PREC_SPLIT, TPS_SPLIT, VEC, ACT>), grid, dim3(256), 0, s, Q);
@@ -587,8 +599,9 @@ static int launch_opconv(const OpConvDev& P, int B, int prec, bool act, double f
     char name[128];
     // the demangled rocprofv3 name of the instantiation (bench.py joins the two by name)
     const int tps = (prec == PREC_SPLIT && BN >= 192) ? 1 : TPS;
-    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %d, %s, %s>", BM, BN, WGM, WGN, prec,
-                  tps, (vec || act) ? "true" : "false", act ? "true" : "false");
+    const bool act3 = act && BM == 128 && prec == PREC_F16 && !P.res;
+    std::snprintf(name, sizeof(name), "alcm::opconv_kernel<%d, %d, %d, %d, %d, %d, %s, %s, %s>", BM, BN, WGM, WGN, prec,
+                  tps, (vec || act) ? "true" : "false", act ? "true" : "false", act3 ? "true" : "false");
     prof_stop(tok, s, name, flops, bytes);
   }
   return 0;
