@@ -472,10 +472,14 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
 #pragma unroll
               for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][1];
           } else {
+            // raised priority while this wave issues its MFMA block, so the co-resident workgroup's waves (in their
+            // staging / epilogue phases) do not interleave VALU work into it (-2..-5 % on the k11 shapes)
+            __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
               for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+            __builtin_amdgcn_s_setprio(0);
           }
         }
         if constexpr (no_sync) continue;
