@@ -371,7 +371,10 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
 // boundary (the stall is covered by the other workgroup).
 constexpr int W2_BM = 128, W2_BN = 192, W2_WROWS = 192;
 
-template <int PREC, bool GEGLU, int AB = 0>
+// ACT (ALCM_WIDE_ACT_FUSION): fused Activation1d epilogue (alcm_actepi.h) — tiles of 128 conv rows emit the middle
+// 112 (tstride 112, tshift 8), v = conv + bias (+ res) staged per 96-column half in LDS, fp32 out for owned rows,
+// Activation1d of owned rows written into the next conv's operand planes
+template <int PREC, bool GEGLU, int AB = 0, bool ACT = false>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   constexpr int WBUF = W2_WROWS * 128;   // window image (24 KB)
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     nt = wid - mt * P.tiles_n;
   }
   const int b = mt / P.tiles_per_batch;
-  const int t0 = (mt - b * P.tiles_per_batch) * W2_BM;
+  const int t0 = (mt - b * P.tiles_per_batch) * P.tstride - P.tshift;
   const int col0 = nt * W2_BN;
   const int K = P.ksize, Cp = P.Cp;
   const int WR = W2_BM + (K - 1) * P.dil;
@@ -504,6 +507,56 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     return;
   }
 
+  if constexpr (ACT) {
+    constexpr int HC = W2_BN / 2;  // the 96 columns of the waves with wn == h
+    constexpr int AOTS = HC + 4;
+    constexpr int acq = HC / 4;
+    float* aot = reinterpret_cast<float*>(smem);  // 128 x 100 floats (51 KB): the K loop's last barrier retired it
+    const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
+    for (int h = 0; h < 2; ++h) {
+      if (wn == h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int nl = j * 16 + (lane & 15);
+              aot[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * AOTS + nl] =
+                  acc[i][j][r] + (P.bias ? P.bias[col0 + h * HC + nl] : 0.f);
+            }
+      }
+      __syncthreads();
+      if (P.res || P.out) {
+        for (int e = tid; e < W2_BM * acq; e += 256) {
+          const int m = e / acq, n = (e - m * acq) * 4;
+          const int t = t0 + m;
+          if (t < 0 || t >= P.T) continue;
+          const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + h * HC + n;
+          float4 v = *reinterpret_cast<const float4*>(aot + m * AOTS + n);
+          if (P.res) {
+            const float4 rv = *reinterpret_cast<const float4*>(P.res + go);
+            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+            *reinterpret_cast<float4*>(aot + m * AOTS + n) = v;
+          }
+          if (P.out && t >= e_lo && t < e_hi) {
+            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+            if (P.accumulate) {
+              const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
+              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+            }
+            *reinterpret_cast<float4*>(P.out + go) = v;
+          }
+        }
+        __syncthreads();
+      }
+      // 112 emitted rows: runs of 14 (8 runs x 48 channel pairs)
+      act_epilogue_tile<PREC, 14>(aot, AOTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 256);
+      __syncthreads();
+    }
+    return;
+  }
+
   // epilogue: one 64-row half of the tile at a time through LDS (the K loop's last barrier retired every
   // fragment read and DMA), whole 768-B row segments with 16-B loads / stores
   constexpr int OTS = W2_BN + 4;
@@ -592,7 +645,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
-  if ((var == 8 || strided) && !act && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
+  if ((var == 8 || strided) && !(act && strided) && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
@@ -602,14 +655,18 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     P.ostride = strided ? a.out_stride : 1;
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;
-    P.ablate = knobs().wconv_ablate;
+    P.ablate = act ? 0 : knobs().wconv_ablate;
+    // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 128 conv rows and emits the middle 112
+    P.tstride = act ? W2_BM - 2 * ACT_EPI_HALO : W2_BM;
+    P.tshift = act ? ACT_EPI_HALO : 0;
+    if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
     // N-tile-major order where the weight matrix is long (Cp * k >= 4096) and there are enough M tiles to share
     // an XCD's weight slice: that XCD's N tiles stay in its L2 (C768 k11 -17 %, DiT FFN -3..-10 %); M-major
     // elsewhere (the N tiles of an M tile share its input window in L2)
-    const int tiles_m = a.B * ((a.T + W2_BM - 1) / W2_BM);
+    const int tiles_m = a.B * ((a.T + P.tstride - 1) / P.tstride);
     const int ord = knobs().wconv_order;
     P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && tiles_m >= 128);
-    P.tiles_per_batch = (a.T + W2_BM - 1) / W2_BM;
+    P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
     P.tiles_n = a.N / W2_BN;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
     if (nwg2 >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
@@ -617,7 +674,10 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     void* tok = prof_start(s);
     const dim3 grid((unsigned)nwg2), blk(256);
     const bool gl = a.geglu_plane != nullptr;
-    if (a.prec == PREC_F16 && !gl && P.ablate) {
+    if (act) {
+      if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 0, true>), grid, blk, 0, s, P);
+      else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, 0, true>), grid, blk, 0, s, P);
+    } else if (a.prec == PREC_F16 && !gl && P.ablate) {
       switch (P.ablate) {
         case 1: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 1>), grid, blk, 0, s, P); break;
         case 2: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 2>), grid, blk, 0, s, P); break;
@@ -638,7 +698,8 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     }
     if (tok) {
       char name[96];
-      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s>", a.prec, gl ? "true" : "false");
+      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s%s>", a.prec, gl ? "true" : "false",
+                    act ? ", 0, true" : "");
       if (knobs().prof_shapes)
         std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp,
                       a.N, a.ksize);
