@@ -617,9 +617,10 @@ bool opconv_act_supported(int prec, int N, int Cp_in) {
   if (knobs().no_act_fusion) return false;  // diagnostics / A-B
   if (N % 4 || N <= 0) return false;
   if (N <= 96) return true;  // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%
-  // wide layers (wconv, one 512-thread workgroup per CU): the activation's VALU work in the epilogue is
-  // serialised with the MFMA K loop and measured slower than the standalone act_op kernel,
-  // so it is opt-in (ALCM_WIDE_ACT_FUSION=1) for A/B runs
+  // wide layers (the two-workgroup wide conv's ACT epilogue, alcm_wconv.hip): the activation's VALU work in the
+  // epilogue does not hide behind the co-resident workgroup's K loop and the 112-of-128-row tiles add 14 % MFMA
+  // work; measured -6 % end to end against conv + standalone cooperative Activation1d, so it is
+  // opt-in (ALCM_WIDE_ACT_FUSION=1) for A/B runs
   if (!knobs().wide_act_fusion) return false;
   return (prec == PREC_F16 || prec == PREC_BF16) && Cp_in % 64 == 0 && (N % 192 == 0 || N % 128 == 0);
 }
