@@ -698,8 +698,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     }
     if (tok) {
       char name[96];
-      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s%s>", a.prec, gl ? "true" : "false",
-                    act ? ", 0, true" : "");
+      // the demangled rocprofv3 name (template defaults included), so bench.py can join the PMC passes by name
+      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s, 0, %s>", a.prec, gl ? "true" : "false",
+                    act ? "true" : "false");
       if (knobs().prof_shapes)
         std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp,
                       a.N, a.ksize);
