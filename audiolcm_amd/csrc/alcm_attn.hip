@@ -248,19 +248,37 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
   const int nqb = (L + 15) / 16, nkt = Lp / FA_KT;
   for (int qb = wave; qb < nqb; qb += FR_THREADS / 64) {
     const int q0 = qb * 16;
+    // (branch-free: clamped addresses and selects; exec-masked loads inside this loop serialise it)
     bf16x8 qf[3];
     {
       const int q = q0 + cq;
+      const bool qok = q < L;
+      const float* qr = base + (int64_t)(qok ? q : 0) * rs;
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) {
         u16 e[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int d = 32 * ks + 8 * g + j;
-          e[j] = fa_cvt<PREC>((q < L && d < dh) ? base[(int64_t)q * rs + d] : 0.f);
+          const float v = qr[d < dh ? d : 0];
+          e[j] = fa_cvt<PREC>((qok && d < dh) ? v : 0.f);
         }
         qf[ks] = __builtin_bit_cast(bf16x8, e);
       }
+    }
+    // K fragment offsets: dims 32 ks + 8 g .. + 7; the slices beyond the 80-element row (ks = 2, g >= 2) read
+    // the zero dims 72 .. 79 instead
+    int koff[3];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) koff[ks] = (32 * ks + 8 * g < FR_KS) ? 32 * ks + 8 * g : FR_MAXDH;
+    // V^T rows >= dh read row dh - 1 and are masked to zero
+    int vrow[5];
+    uint32_t vmask[5];
+#pragma unroll
+    for (int db = 0; db < 5; ++db) {
+      const int r = 16 * db + cq;
+      vrow[db] = (r < dh ? r : dh - 1) * VS;
+      vmask[db] = r < dh ? 0xffffffffu : 0u;
     }
     f32x4 o[5];
 #pragma unroll
@@ -274,9 +292,7 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
         s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
-          // dims 32 ks + 8 g .. + 7 beyond the 80-element row are zero (only ks = 2, g >= 2)
-          bf16x8 kf = bf16x8{};
-          if (ks < 2 || g < 2) kf = *reinterpret_cast<const bf16x8*>(&Ks[(k0 + 16 * kb + cq) * FR_KS + 32 * ks + 8 * g]);
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(k0 + 16 * kb + cq) * FR_KS + koff[ks]]);
           s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
         }
       }
@@ -318,13 +334,11 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
         const bf16x8 pf = __builtin_bit_cast(bf16x8, pe);
 #pragma unroll
         for (int db = 0; db < 5; ++db) {
-          uint4 vv = make_uint4(0u, 0u, 0u, 0u);  // V^T rows >= dh are zero
-          if (16 * db + cq < dh) {
-            const u16* vr = &Vt[(16 * db + cq) * VS + k0 + 32 * ks + 4 * g];
-            const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-            const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
-            vv = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          }
+          const u16* vr = &Vt[vrow[db] + k0 + 32 * ks + 4 * g];
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          const uint32_t mk = vmask[db];
+          const uint4 vv = make_uint4(lo.x & mk, lo.y & mk, hi.x & mk, hi.y & mk);
           o[db] = mfma16<PREC>(__builtin_bit_cast(bf16x8, vv), pf, o[db]);
         }
       }

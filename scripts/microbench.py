@@ -283,6 +283,14 @@ def bench_tail(B=32):
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
 
 
+def bench_attn(B=32):
+    """DiT self-attention at the bench shape (L = 467, 8 heads x 72), fp16 operands"""
+    L, H = 467, 576
+    qkv = torch.randn((B, L, 3 * H), device="cuda")
+    ms = timeit(lambda: K.flash_attention(qkv, 8, 2), reps=20)
+    print(f"attn B={B} L={L}: {ms * 1e3:.1f} us ({B * L * 3 * H * 4 / 1e9 / ms:.2f} TB/s of qkv)", flush=True)
+
+
 def bench_act1(B=32):
     """one standalone Activation1d launch (C = 384 stage-1 shape, fp16 planes) and one fused tail conv (C = 96 k11,
     residual + Activation1d epilogue), 3 launches each (target of rocprofv3 --pmc passes)"""
@@ -324,4 +332,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
