@@ -2,9 +2,10 @@
 
 Mirrors the reference CLI (scripts/txt2audio_for_lcm.py:48-152 arguments, :209-270 main) — the same flags,
 output names and ``result.csv`` — with every model stage in libaudiolcm_hip.  Differences, all deliberate:
-  * prompts are generated in batches (``--batch-size``, the reference loops at batch 1) with per-prompt RNG
-    seeds (``--seed`` + prompt index; the reference draws from the global RNG), so outputs do not depend on
-    the batching;
+  * prompts are generated in batches (``--batch-size``, the reference loops at batch 1) with per-clip RNG
+    seeds derived from the global prompt index, the iteration and the sample
+    (``--seed + (prompt * n_iter + iteration) * n_samples + sample``; the reference draws from the global RNG),
+    so outputs do not depend on the batching;
   * ``--prompt_txt`` lines become ``{'ori_caption': p, 'struct_caption': '<p& all>'}`` as InferAPI.py:137 builds
     them (the reference passes the raw string to ``gen_test_sample``, which fails on ``prompt.items()``);
   * the unused unconditional embedding (``uc``, computed when ``--scale != 1`` and never passed to the LCM
@@ -49,6 +50,8 @@ def parse_args(argv: Optional[Sequence[str]] = None):
     p.add_argument("--vocoder-ckpt", type=str, default="vocoder/logs/audioset", help="path to vocoder checkpoint")
     # MI355X build options
     p.add_argument("--synthetic-seed", type=int, default=None, help="run on the seeded synthetic recipe weights")
+    p.add_argument("--synthetic-tokenizer", action="store_true",
+                   help="with -r: use the hash-id tokenizer stand-in when the tokenizer directories are absent")
     p.add_argument("--batch-size", type=int, default=32, help="prompts per batched generation")
     p.add_argument("--seed", type=int, default=0, help="per-prompt RNG seeds are seed + prompt index")
     p.add_argument("--precision", choices=["split", "mixed", "bf16"], default="mixed",
@@ -67,11 +70,14 @@ class GenSamples:
         self.save_mel, self.save_wav = save_mel, save_wav
         self.channel_dim = model.channels
         self.original_inference_steps = original_inference_steps
-        self.next_seed = opt.seed
 
-    def gen_batch(self, prompts: List[Dict[str, str]], names: List[str]) -> List[Dict[str, str]]:
-        """prompts[i] -> n_iter x n_samples clips named <names[i]>_<idx>; returns the records in the reference's
-        order (per prompt, per iteration, per sample)."""
+    def clip_seed(self, prompt_index: int, it: int, j: int) -> int:
+        """RNG seed of sample j of iteration `it` of the prompt at global index `prompt_index` (batch-invariant)."""
+        return self.opt.seed + (prompt_index * self.opt.n_iter + it) * self.opt.n_samples + j
+
+    def gen_batch(self, prompts: List[Dict[str, str]], names: List[str], first_index: int = 0) -> List[Dict[str, str]]:
+        """prompts[i] (global prompt index first_index + i) -> n_iter x n_samples clips named <names[i]>_<idx>;
+        returns the records in the reference's order (per prompt, per iteration, per sample)."""
         n = self.opt.n_samples
         records: List[List[Dict[str, str]]] = [[] for _ in prompts]
         for it in range(self.opt.n_iter):
@@ -79,8 +85,7 @@ class GenSamples:
                     "struct_caption": [p["struct_caption"] for p in prompts for _ in range(n)]}
             c = self.model.get_learned_conditioning(text)
             B = c.shape[0]
-            seeds = list(range(self.next_seed, self.next_seed + B))
-            self.next_seed += B
+            seeds = [self.clip_seed(first_index + i, it, j) for i in range(len(prompts)) for j in range(n)]
             shape = [self.channel_dim, self.opt.H, self.opt.W] if self.channel_dim > 0 else [self.opt.H, self.opt.W]
             z, _ = self.sampler.sample(S=self.opt.ddim_steps, conditioning=c, batch_size=B, shape=shape,
                                        verbose=False, guidance_scale=self.opt.scale,
@@ -122,6 +127,8 @@ def build(opt):
             raise FileNotFoundError(f"checkpoint {opt.resume!r} not found (pass --synthetic-seed N to run on the "
                                     "seeded synthetic weights)")
         model = load_model_from_config(config, opt.resume, split=split)
+        if opt.synthetic_tokenizer and model.cond_stage_model is not None:
+            model.cond_stage_model.use_synthetic_tokenizer()
         if "bigv" not in opt.vocoder_ckpt:
             raise NotImplementedError(f"vocoder {opt.vocoder_ckpt!r}: only BigVGAN checkpoints are on the path")
         vocoder = VocoderBigVGAN(opt.vocoder_ckpt, split=split)
@@ -145,17 +152,17 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Dict[str, str]]:
             if opt.test_dataset_tsv:
                 dcfg["params"] = dict(dcfg.get("params", {}), tsv_path=opt.test_dataset_tsv)
             test_dataset = instantiate_from_config(dcfg)
+            test_dataset.load_mel = False  # ground-truth mels are for evaluation only
             print(f"Dataset: {type(test_dataset)} LEN: {len(test_dataset)}")
-            items = list(test_dataset)
-            for lo in range(0, len(items), bs):
+            for lo in range(0, len(test_dataset), bs):
                 prompts, names = [], []
-                for item in items[lo:lo + bs]:
+                for item in (test_dataset[i] for i in range(lo, min(lo + bs, len(test_dataset)))):
                     f_name = item["f_name"]
                     cut = f_name.rfind("_")  # file name = video_name + '_' + num
                     v_n, num = f_name[:cut], f_name[cut + 1:]
                     prompts.append(dict(item["caption"]))
                     names.append(f"{v_n}_sample_{num}")
-                csv_dicts.extend(gen.gen_batch(prompts, names))
+                csv_dicts.extend(gen.gen_batch(prompts, names, lo))
             import pandas as pd
             pd.DataFrame.from_dict(csv_dicts).to_csv(os.path.join(opt.outdir, "result.csv"), sep="\t", index=False)
         else:
@@ -164,7 +171,7 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Dict[str, str]]:
             for lo in range(0, len(lines), bs):
                 chunk = lines[lo:lo + bs]
                 csv_dicts.extend(gen.gen_batch([dict(ori_caption=p, struct_caption=struct_caption(p)) for p in chunk],
-                                               [p.replace(" ", "-") for p in chunk]))
+                                               [p.replace(" ", "-") for p in chunk], lo))
     print(f"Your samples are ready and waiting four you here: \n{opt.outdir} \nEnjoy.")
     return csv_dicts
 

@@ -1326,8 +1326,11 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // scripts/precision_emulate.py 96 tail) take a plane conv of x with a strided epilogue (the wide-layer
     // kernel for N % 192 == 0, opconv_kernel for N <= 96); the others the fp32-operand conv at the base
     // precision
+    // (the same eligibility opconv's strided paths check: the wide-layer kernel needs Cp % 64 == 0 and a tap
+    // window of at most 64 rows; otherwise the fp32-operand phase conv below, never a hard error)
+    const bool wide_ok = S.cout % 192 == 0 && S.cin % 64 == 0 && S.phase[0].w.taps - 1 <= 64;
     const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cin % 32 == 0 &&
-                            (S.cout % 192 == 0 || (S.cout <= 96 && S.cout % 4 == 0)) &&
+                            (wide_ok || (S.cout <= 96 && S.cout % 4 == 0)) &&
                             S.phase[0].w.cpad == S.cin && !knobs().ups_fp32;
     if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
     for (int r = 0; r < S.rate; ++r) {
@@ -1634,7 +1637,9 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
     ALCM_TRY(conv(s, pl, 1, R, View{w.x, 0, D, 1, R, D}, Bk.wi, Out{w.inter, 0, X.t_ff, 1, 1, 0}, of));
     ConvOpts r2;
     r2.res = Res{w.x, 0, D, 1};
-    ALCM_TRY(lin(s, pl, R, w.inter, X.t_ff, Bk.wo, w.x, r2));
+    // wo reads the gated-GELU product, which exceeds the fp16 range on real T5 v1.1 weights (transformers keeps
+    // this layer in fp32 for that reason): bf16 hi/lo operands (fp32 range) under every non-bf16 policy
+    ALCM_TRY(lin(s, ps, R, w.inter, X.t_ff, Bk.wo, w.x, r2));
   }
   return rms_norm(w.x, R, D, X.t_eps, X.t_fin, L, (int64_t)2 * L * D, out + (int64_t)L * D, s);
 }

@@ -18,9 +18,10 @@ import numpy as np
 
 
 class TSVDataset:
-    def __init__(self, tsv_path: str, spec_crop_len: Optional[int] = None):
+    def __init__(self, tsv_path: str, spec_crop_len: Optional[int] = None, load_mel: bool = True):
         import pandas as pd
         self.batch_max_length = spec_crop_len
+        self.load_mel = load_mel  # generation (the CLI's dataset mode) never reads the ground-truth mel
         df = pd.read_csv(tsv_path, sep="\t")
         self.dataset = self.add_name_num(df)
         self.root = os.path.dirname(os.path.abspath(tsv_path))
@@ -39,7 +40,7 @@ class TSVDataset:
         return df
 
     def _mel(self, path) -> Optional[np.ndarray]:
-        if not isinstance(path, str):
+        if not self.load_mel or not isinstance(path, str):
             return None
         p = path if os.path.isabs(path) or os.path.exists(path) else os.path.join(self.root, path)
         if not os.path.exists(p):

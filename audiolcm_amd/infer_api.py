@@ -88,7 +88,7 @@ class GenSamples:
         return self.gen_batch([prompt], [name])
 
 
-def _build(config_path, model_path, vocoder_path, synthetic_seed, split):
+def _build(config_path, model_path, vocoder_path, synthetic_seed, split, synthetic_tokenizer=False):
     config = load_config(config_path)
     if synthetic_seed is None:
         if not model_path or not os.path.exists(model_path):
@@ -97,6 +97,8 @@ def _build(config_path, model_path, vocoder_path, synthetic_seed, split):
         if not vocoder_path or not os.path.exists(os.path.join(vocoder_path, "best_netG.pt")):
             raise FileNotFoundError(f"vocoder checkpoint dir {vocoder_path!r} not found")
         model = load_model_from_config(config, model_path, split=split)
+        if synthetic_tokenizer and model.cond_stage_model is not None:
+            model.cond_stage_model.use_synthetic_tokenizer()
         vocoder = VocoderBigVGAN(vocoder_path, split=split)
     else:
         model = load_model_from_config(config, None, split=split, synthetic_seed=synthetic_seed)
@@ -109,11 +111,14 @@ def _build(config_path, model_path, vocoder_path, synthetic_seed, split):
 def AudioLCMBatchInfer(ori_prompts: List[str], config_path: str = "configs/audiolcm.yaml",
                        model_path: str = "./model/000184.ckpt", vocoder_path: str = "./model/vocoder",
                        batch_size: int = 32, synthetic_seed: Optional[int] = None, split: bool = True,
-                       outpath: str = "results/test", seed: Optional[int] = None) -> str:
+                       outpath: str = "results/test", seed: Optional[int] = None,
+                       synthetic_tokenizer: bool = False) -> str:
     """InferAPI.py:135-166. Returns the path of the last prompt's WAV.  ``seed``: per-prompt RNG seeds
-    seed + i (default None: the global device RNG, as the reference)."""
+    seed + i (default None: the global device RNG, as the reference).  ``synthetic_tokenizer``: run checkpoint
+    weights on the hash-id tokenizer stand-in when the tokenizer directories are absent (tests only)."""
     prompts = [dict(ori_caption=p, struct_caption=struct_caption(p)) for p in ori_prompts]
-    model, sampler, vocoder, orig_steps = _build(config_path, model_path, vocoder_path, synthetic_seed, split)
+    model, sampler, vocoder, orig_steps = _build(config_path, model_path, vocoder_path, synthetic_seed, split,
+                                                 synthetic_tokenizer)
     os.makedirs(outpath, exist_ok=True)
     gen = GenSamples(sampler, model, outpath, vocoder, save_mel=False, save_wav=True,
                      original_inference_steps=orig_steps)

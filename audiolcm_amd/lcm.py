@@ -83,6 +83,8 @@ class LCM_audio:
         self.first_stage_model.load_state_dict(recipe.vae_state(seed))
         if self.cond_stage_model is not None and hasattr(self.cond_stage_model, "load_state_dict"):
             self.cond_stage_model.load_state_dict(recipe.text_state(seed))
+            if hasattr(self.cond_stage_model, "use_synthetic_tokenizer"):  # recipe weights: hash ids are as good
+                self.cond_stage_model.use_synthetic_tokenizer()
         return self
 
     @property

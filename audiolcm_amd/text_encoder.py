@@ -11,10 +11,12 @@ no attention mask is passed, so the padding tokens take part in attention.
 Weights: the reference's checkpoint layout (``cond_stage_model.caption_encoder.base.*`` / ``.projection.*`` /
 ``cond_stage_model.t5_transformer.*``, loaded by LCM_audio.load_state_dict), local HuggingFace model
 directories with ``model.safetensors`` (the reference's ``from_pretrained`` paths), or the seeded recipe.
-Tokenizers: local HuggingFace tokenizer directories when they exist (the reference's ``bert-base-uncased`` /
-``t5-v1_1-large`` paths); otherwise a deterministic stand-in (``SyntheticTokenizer``) that maps words to ids
-by a stable hash — the real vocabularies are not available offline, so token ids are parity-unpinned, while
-the encoders themselves are pinned from ids (tests/golden/text_B2_L77.npz).
+Tokenizers: local HuggingFace tokenizer directories (the reference's ``bert-base-uncased`` / ``t5-v1_1-large``
+paths).  A deterministic stand-in (``SyntheticTokenizer``, words -> ids by a stable hash) is used only on
+request — with the seeded recipe weights (``synthetic_seed`` / ``load_recipe``) or ``synthetic_tokenizer=True`` —
+because real encoder weights fed made-up ids would give silently wrong conditioning; without a loadable tokenizer
+directory and without that opt-in, ``encode`` raises.  The real vocabularies are not available offline, so
+token ids are parity-unpinned, while the encoders themselves are pinned from ids (tests/golden/text_B2_L77.npz).
 """
 from __future__ import annotations
 
@@ -81,7 +83,7 @@ def _hf_tokenizer(path: Optional[str], kind: str):
             from transformers import AutoTokenizer
             return AutoTokenizer.from_pretrained(path)
         except Exception as e:  # pragma: no cover - depends on local files
-            print(f"tokenizer at {path!r} not loadable ({e}); using the synthetic tokenizer")
+            print(f"tokenizer at {path!r} not loadable ({e})")
     return None
 
 
@@ -153,12 +155,15 @@ class FrozenCLAPFLANEmbedder:
     def __init__(self, weights_path=None, t5version="../ldm/modules/encoders/CLAP/t5-v1_1-large", freeze=True,
                  device="cuda", max_length=77, text_model="../ldm/modules/encoders/CLAP/bert-base-uncased",
                  synthetic_seed: Optional[int] = None, split=True, cfg: Optional[recipe.TextConfig] = None,
-                 **unused):
+                 synthetic_tokenizer: bool = False, **unused):
         self.max_length = max_length
         self.device = device
         self.cfg = cfg or recipe.TextConfig(max_len=max_length)
-        self.clap_tokenizer = _hf_tokenizer(text_model, "bert") or SyntheticTokenizer("bert", self.cfg.b_vocab)
-        self.t5_tokenizer = _hf_tokenizer(t5version, "t5") or SyntheticTokenizer("t5", self.cfg.t_vocab)
+        self.tokenizer_paths = (text_model, t5version)
+        self.clap_tokenizer = _hf_tokenizer(text_model, "bert")
+        self.t5_tokenizer = _hf_tokenizer(t5version, "t5")
+        if synthetic_tokenizer or synthetic_seed is not None:
+            self.use_synthetic_tokenizer()
         self.model = CLAPT5TextEncoder(self.cfg, split=split)
         state = {}
         if text_model and os.path.isdir(text_model):
@@ -178,10 +183,21 @@ class FrozenCLAPFLANEmbedder:
         self._pending = {}
         return self
 
+    def use_synthetic_tokenizer(self):
+        """Opt in to the hash stand-in for whichever tokenizer directory is missing (recipe weights / tests)."""
+        self.clap_tokenizer = self.clap_tokenizer or SyntheticTokenizer("bert", self.cfg.b_vocab)
+        self.t5_tokenizer = self.t5_tokenizer or SyntheticTokenizer("t5", self.cfg.t_vocab)
+        return self
+
     def set_split(self, split):
         self.model.set_split(split)
 
     def tokenize(self, ori_caption: Sequence[str], struct_caption: Sequence[str]):
+        if self.clap_tokenizer is None or self.t5_tokenizer is None:
+            missing = [p for p, t in zip(self.tokenizer_paths, (self.clap_tokenizer, self.t5_tokenizer)) if t is None]
+            raise RuntimeError(f"FrozenCLAPFLANEmbedder: no loadable HuggingFace tokenizer at {missing!r}; real "
+                               "encoder weights need the real vocabularies (pass text_model= / t5version= tokenizer "
+                               "directories, or synthetic_tokenizer=True to run the hash stand-in deliberately)")
         kw = dict(truncation=True, max_length=self.max_length, return_length=True, return_overflowing_tokens=False,
                   padding="max_length", return_tensors="pt")
         return self.clap_tokenizer(list(ori_caption), **kw)["input_ids"], \

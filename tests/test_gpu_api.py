@@ -64,8 +64,10 @@ def test_checkpoint_ingestion_matches_recipe(gpu, tmp_path):
     (vd / "args.yml").write_text(yaml.safe_dump(BIGVGAN_ARGS))
     prompts = ["a dog barks", "rain falls on a tin roof"]
     out_ck, out_rc = tmp_path / "ck", tmp_path / "rc"
+    with pytest.raises(RuntimeError, match="tokenizer"):  # real-layout weights, no vocabulary: refuse, don't guess
+        AudioLCMBatchInfer(prompts, config_path=CFG, model_path=mp, vocoder_path=str(vd), outpath=str(out_ck), seed=7)
     p1 = AudioLCMBatchInfer(prompts, config_path=CFG, model_path=mp, vocoder_path=str(vd), outpath=str(out_ck),
-                            seed=7)
+                            seed=7, synthetic_tokenizer=True)
     p2 = AudioLCMBatchInfer(prompts, config_path=CFG, synthetic_seed=0, outpath=str(out_rc), seed=7)
     assert os.path.basename(p1) == os.path.basename(p2) == "rain-falls-on-a-tin-roof_0.wav"
     for p in prompts:

@@ -47,6 +47,45 @@ def test_text_encode_mixed_policy(enc):
     assert err < 3e-3
 
 
+def test_text_encode_mixed_t5_ffn_beyond_fp16_range():
+    """T5 v1.1 FFN activations exceed 65504 on real weights (transformers keeps DenseReluDense.wo in fp32).  Scale
+    the recipe's wi_0 / wi_1 by 150 (and wo by 1/150^2) so block 0's wo input peaks far above the fp16 range: the
+    mixed policy must stay finite and within its 3e-3 tolerance of the fp32 oracle."""
+    import torch.nn.functional as F
+    from audiolcm_amd import recipe
+    from audiolcm_amd.text_encoder import CLAPT5TextEncoder
+    from oracle import alcm_oracle as O
+    s = 150.0
+    W = dict(recipe.text_state(0))
+    for k in list(W):
+        if ".DenseReluDense.wi_" in k:
+            W[k] = W[k] * s
+        elif ".DenseReluDense.wo." in k:
+            W[k] = W[k] / (s * s)
+    g = golden("text_B2_L77.npz")
+    a, b = torch.from_numpy(g["clap_ids"]), torch.from_numpy(g["t5_ids"])
+    # block 0's wo input, restated from the oracle's T5 block (alcm_oracle.t5_encoder_forward)
+    p, q = "t5_transformer.", "t5_transformer.encoder.block.0.layer."
+    rms = lambda t, w: w * (t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + 1e-6))
+    tab = W[q + "0.SelfAttention.relative_attention_bias.weight"]
+    bias = tab[O.t5_relative_bucket(b.shape[1], tab.shape[0])].permute(2, 0, 1)[None]
+    x = W[p + "shared.weight"][b]
+    h = rms(x, W[q + "0.layer_norm.weight"])
+    att = O._mha(*(F.linear(h, W[q + f"0.SelfAttention.{n}.weight"]) for n in "qkv"), 16, 1.0, bias)
+    h = rms(x + F.linear(att, W[q + "0.SelfAttention.o.weight"]), W[q + "1.layer_norm.weight"])
+    u = F.gelu(F.linear(h, W[q + "1.DenseReluDense.wi_0.weight"]), approximate="tanh") * \
+        F.linear(h, W[q + "1.DenseReluDense.wi_1.weight"])
+    assert float(u.abs().max()) > 2 * 65504.0
+    with torch.no_grad():
+        ref = O.text_encode(W, a, b).numpy()
+    m = CLAPT5TextEncoder(split="mixed").load_state_dict(W)
+    out = m.encode_ids(a, b).cpu().numpy()
+    assert np.isfinite(out).all()
+    err = rel_l2(out, ref)
+    print(f"text mixed, T5 FFN x{s}: {err:.2e}")
+    assert err < 3e-3
+
+
 def test_text_encode_short_sequence_and_batch_invariance(enc, states_text):
     """L = 20 (< max_length: the relative-bias sub-block) vs the oracle, and prompt 1 alone == in a batch of 3."""
     from oracle import alcm_oracle as O
@@ -73,7 +112,7 @@ def test_embedder_encode_captions(enc):
     """FrozenCLAPFLANEmbedder.encode on caption dicts (synthetic tokenizer stand-in) == encode_ids of the
     tokenizer's ids, (B, 154, 1024), finite."""
     from audiolcm_amd.text_encoder import FrozenCLAPFLANEmbedder
-    emb = FrozenCLAPFLANEmbedder(weights_path=None, t5version=None, text_model=None)
+    emb = FrozenCLAPFLANEmbedder(weights_path=None, t5version=None, text_model=None, synthetic_tokenizer=True)
     emb.model = enc
     caps = ["a dog barks", "rain falls on a tin roof"]
     text = {"ori_caption": caps, "struct_caption": [f"<{c}& all>" for c in caps]}

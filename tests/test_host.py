@@ -185,7 +185,12 @@ def test_yaml_instantiates_lcm_model_without_gpu():
     assert isinstance(m.first_stage_model, models.AutoencoderKL)
     assert m.first_stage_model.cfg.upsample_levels == (1,)
     assert isinstance(m.cond_stage_model, text_encoder.FrozenCLAPFLANEmbedder)
-    assert isinstance(m.cond_stage_model.clap_tokenizer, text_encoder.SyntheticTokenizer)  # no vocab offline
+    assert m.cond_stage_model.clap_tokenizer is None  # no vocabulary offline, and no silent stand-in
+    with pytest.raises(RuntimeError, match="tokenizer"):
+        m.cond_stage_model.tokenize(["a dog barks"], ["<a dog barks& all>"])
+    m.cond_stage_model.use_synthetic_tokenizer()  # explicit opt-in (recipe weights / tests)
+    a, b = m.cond_stage_model.tokenize(["a dog barks"], ["<a dog barks& all>"])
+    assert a.shape == b.shape == (1, 77)
     assert not m.cond_stage_model.model.loaded
     assert not m.unet.diffusion_model.loaded
     with pytest.raises(RuntimeError):
@@ -278,6 +283,41 @@ def test_cli_arguments_match_reference():
     o = parse_args(["--test-dataset", "audiocaps", "--ddim_steps", "2", "-r", "x.ckpt", "-b", "c.yaml",
                     "--vocoder-ckpt", "bigvgan", "--sample_rate", "16000"])
     assert o.test_dataset == "audiocaps" and o.ddim_steps == 2 and o.resume == "x.ckpt" and o.base == "c.yaml"
+
+
+class _StubSampler:
+    def __init__(self):
+        self.seeds = []
+
+    def sample(self, S, conditioning, batch_size, shape, seeds, **kw):
+        self.seeds.extend(seeds)
+        return torch.tensor(seeds, dtype=torch.float32)[:, None], None
+
+
+class _StubModel:
+    channels = 0
+
+    def get_learned_conditioning(self, text):
+        return torch.zeros(len(text["ori_caption"]), 1)
+
+    def decode_first_stage(self, z):
+        return z
+
+
+def test_cli_seeds_do_not_depend_on_batching():
+    """Per-clip seeds come from (global prompt index, iteration, sample), so --batch-size 1 and 4 give every clip
+    the same seed with --n_iter 2 --n_samples 2 (a running counter made them depend on the chunking)."""
+    from audiolcm_amd.cli import GenSamples, parse_args
+    prompts = [dict(ori_caption=f"p{i}", struct_caption=f"<p{i}& all>") for i in range(5)]
+    per_clip = []
+    for bs in (1, 4):
+        opt = parse_args(["--n_iter", "2", "--n_samples", "2", "--seed", "11"])
+        samp = _StubSampler()
+        gen = GenSamples(opt, samp, _StubModel(), "/nonexistent", None, save_mel=False, save_wav=False)
+        for lo in range(0, len(prompts), bs):
+            gen.gen_batch(prompts[lo:lo + bs], [p["ori_caption"] for p in prompts[lo:lo + bs]], lo)
+        per_clip.append(sorted(samp.seeds))
+    assert per_clip[0] == per_clip[1] == list(range(11, 11 + 5 * 2 * 2))
 
 
 class _HParams:  # stands in for a Lightning checkpoint's OmegaConf / Namespace hyper_parameters
