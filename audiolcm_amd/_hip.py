@@ -60,7 +60,8 @@ class NamedTensor(C.Structure):
 
 class ProfEntry(C.Structure):
     _fields_ = [("name", C.c_char * 128), ("launches", i64), ("total_ms", C.c_double), ("flops", C.c_double),
-                ("bytes", C.c_double), ("roof_ms", C.c_double)]
+                ("bytes", C.c_double), ("roof_ms", C.c_double), ("hbm_launches", i64), ("hbm_ms", C.c_double),
+                ("hbm_bytes", C.c_double)]
 
 
 # (name, restype, argtypes) — every symbol include/audiolcm_hip.h declares
@@ -177,10 +178,12 @@ def profile_begin(peak_flops: float = PEAK_BF16_FLOPS, peak_bytes: float = PEAK_
 
 
 def profile_end(max_entries: int = 256):
-    """-> list of dicts {name, launches, total_ms, flops, bytes} (synchronises the recorded events)."""
+    """-> list of dicts {name, launches, total_ms, flops, bytes, roof_ms, hbm_launches, hbm_ms, hbm_bytes}
+    (synchronises the recorded events; hbm_* aggregate the launches whose algorithmic intensity is HBM-bound)."""
     arr = (ProfEntry * max_entries)()
     n = C.c_int(0)
     check(lib().alcm_profile_end(arr, max_entries, C.byref(n)), "alcm_profile_end")
     return [dict(name=arr[i].name.decode(), launches=int(arr[i].launches), total_ms=float(arr[i].total_ms),
-                 flops=float(arr[i].flops), bytes=float(arr[i].bytes), roof_ms=float(arr[i].roof_ms))
+                 flops=float(arr[i].flops), bytes=float(arr[i].bytes), roof_ms=float(arr[i].roof_ms),
+                 hbm_launches=int(arr[i].hbm_launches), hbm_ms=float(arr[i].hbm_ms), hbm_bytes=float(arr[i].hbm_bytes))
             for i in range(min(n.value, max_entries))]

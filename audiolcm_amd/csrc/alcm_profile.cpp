@@ -77,6 +77,8 @@ extern "C" int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_en
   struct Agg {
     int64_t n = 0;
     double ms = 0, flops = 0, bytes = 0, roof = 0;
+    int64_t hn = 0;
+    double hms = 0, hbytes = 0;
   };
   std::map<std::string, Agg> agg;
   for (auto& r : g_recs) {
@@ -89,6 +91,11 @@ extern "C" int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_en
     a.flops += r.flops;
     a.bytes += r.bytes;
     a.roof += 1e3 * std::max(r.flops / g_pf, r.bytes / g_pb);
+    if (r.flops * g_pb < r.bytes * g_pf) {  // HBM-bound by its algorithmic intensity
+      a.hn += 1;
+      a.hms += ms;
+      a.hbytes += r.bytes;
+    }
   }
   int i = 0;
   for (auto& kv : agg) {
@@ -99,6 +106,9 @@ extern "C" int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_en
       out[i].flops = kv.second.flops;
       out[i].bytes = kv.second.bytes;
       out[i].roof_ms = kv.second.roof;
+      out[i].hbm_launches = kv.second.hn;
+      out[i].hbm_ms = kv.second.hms;
+      out[i].hbm_bytes = kv.second.hbytes;
     }
     ++i;
   }

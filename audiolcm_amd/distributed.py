@@ -25,17 +25,41 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
-    """torch.distributed init from RANK/WORLD_SIZE/LOCAL_RANK (torchrun); returns (rank, world, local)."""
+def init_from_env(backend: Optional[str] = None, device: Optional[int] = None) -> Tuple[int, int, int]:
+    """torch.distributed init from RANK/WORLD_SIZE/LOCAL_RANK (torchrun); returns (rank, world, local).
+
+    ``device``: the GPU this rank drives.  It is made current BEFORE the process group exists and, for
+    nccl (RCCL), bound to the group (``device_id``), so collectives and barriers never guess a device."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device is not None:
+        torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group(backend=backend or ("nccl" if torch.cuda.is_available() else "gloo"),
-                                rank=rank, world_size=world)
+        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        kw = {}
+        if backend == "nccl" and device is not None:
+            kw["device_id"] = torch.device("cuda", device)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, world, local
+
+
+def barrier(group=None) -> None:
+    """dist.barrier on the rank's own device for nccl (no device guess), plain for gloo."""
+    if dist.get_backend(group) == "nccl":
+        dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier(group=group)
+
+
+def all_reduce_max(value: float, group=None) -> float:
+    """Max of a host scalar over ranks (bench timing): on the device for nccl, on the host for gloo."""
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
 
 
 def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
@@ -49,7 +73,12 @@ def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tens
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
     out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
+    if local.is_cuda and dist.get_backend(group) != "nccl":  # gloo (device-map rehearsals): through the host
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(host, pad.cpu(), group=group)
+        out.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out, pad, group=group)
     rows = [out[r * per: r * per + (shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0])]
             for r in range(world)]
     return torch.cat(rows, 0)

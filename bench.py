@@ -50,11 +50,44 @@ def parse():
                          "everywhere (fp32 parity); bf16 = one bf16 MFMA everywhere (misses the parity bar)")
     ap.add_argument("--also-other-mode", type=int, default=1, help="N=1: also time the other precision policies")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-clips", type=int, default=1, help="clips per timed CPU run (median of 3 runs)")
+    ap.add_argument("--cpu-clips", type=int, default=4,
+                    help="prompts in the one batched CPU-oracle run (the bounded sample; 32 = the full configs[1] "
+                         "batch of BASELINE.md §4, ~250 s on 16 EPYC cores, profiles/r3a/bench_default_b32cpu.json)")
+    ap.add_argument("--dist-backend", default=None, help="N>1: torch.distributed backend (default nccl = RCCL)")
+    ap.add_argument("--device-map", default=None,
+                    help="N>1 rehearsal: comma-separated GPU index per LOCAL_RANK (default: GPU = LOCAL_RANK)")
+    ap.add_argument("--dump-wav", default=None, help="rank 0: save the gathered waveforms of the last step (.npy)")
     ap.add_argument("--extra-configs", type=int, default=1,
                     help="N=1: also time BASELINE configs[3] (C4: B=64, 4 steps + CFG) and configs[4] (C5: B=16, "
                          "30 s decode) and report them beside the headline")
     return ap.parse_args()
+
+
+def log(msg: str) -> None:
+    """Progress to stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+class Heartbeat:
+    """Prints a progress line every `every` seconds while a long host-side phase runs."""
+
+    def __init__(self, what: str, every: float = 20.0):
+        import threading
+        self.what, self.every, self.t0 = what, every, time.perf_counter()
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: {time.perf_counter() - self.t0:.0f} s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
 
 
 def cpu_model() -> str:
@@ -70,9 +103,12 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(clips: int, latent_len: int, lcm_steps: int):
-    """The oracle (fp32 PyTorch-CPU restatement of the reference path, pinned to the reference's fixtures) on a
-    bounded sample, per BASELINE.md §4: all the cores this process may use, one warm-up, median of 3 runs."""
-    import statistics
+    """The oracle (fp32 PyTorch-CPU restatement of the reference path, pinned to the reference's fixtures) in the
+    form BASELINE.md §4 / SURVEY §8(d) prescribe: `clips` prompts in ONE batched sampler call followed by batched
+    VAE decode and BigVGAN vocode, on every core this job may use.  One untimed warm-up at batch 1 (pages in the
+    code and oneDNN primitives), then one timed batched run.  The default bounded sample is 4 prompts (~30 s);
+    `--cpu-clips 32` runs the full configs[1] batch (measured 1.28 audio-s/s in 250 s on 16 EPYC 9575F threads,
+    profiles/r3a/bench_default_b32cpu.json: batching makes the CPU path slower per clip, not faster)."""
     from audiolcm_amd import recipe
     from oracle import alcm_oracle as O
     cores = len(os.sched_getaffinity(0))
@@ -80,24 +116,29 @@ def cpu_baseline(clips: int, latent_len: int, lcm_steps: int):
     threads = max(1, min(cores, int(share))) if share and share.isdigit() else cores
     torch.set_num_threads(threads)
     Wd, Wv, Wg = recipe.dit_state(0), recipe.vae_state(0), recipe.bigvgan_state(0)
-    ctx = recipe.synthetic_context(clips)
-    xT, noise = recipe.prompt_noise(range(clips), lcm_steps, 20, latent_len)
-
-    def run():
+    ids = list(range(clips))
+    ctx = torch.cat([recipe.synthetic_context(1, seed0=1000 + i) for i in ids], 0)
+    xT, noise = recipe.prompt_noise(ids, lcm_steps, 20, latent_len)
+    with torch.no_grad(), Heartbeat(f"cpu_baseline ({clips} prompts, {threads} threads)"):
         t0 = time.perf_counter()
-        with torch.no_grad():
-            for i in range(clips):  # per clip, as the reference API (InferAPI.py:159-163)
-                O.generate(Wd, Wv, Wg, ctx[i:i + 1], xT[i:i + 1], noise[:, i:i + 1], S=lcm_steps)
-        return time.perf_counter() - t0
-    run()  # warm-up
-    times = [run() for _ in range(3)]
-    dt = statistics.median(times)
+        O.generate(Wd, Wv, Wg, ctx[:1], xT[:1], noise[:, :1], S=lcm_steps)  # warm-up
+        log(f"cpu_baseline warm-up (1 prompt): {time.perf_counter() - t0:.1f} s")
+        t0 = time.perf_counter()
+        O.generate(Wd, Wv, Wg, ctx, xT, noise, S=lcm_steps)  # one batched call: sampler, decode, vocode
+        dt = time.perf_counter() - t0
+        log(f"cpu_baseline batched run: {dt:.1f} s")
     audio = clips * latent_len * 2 * HOP / SR
+    full = os.path.join(HERE, "profiles", "r3a", "bench_default_b32cpu.json")
+    ref32 = None
+    if clips != 32 and os.path.exists(full):
+        rec = json.load(open(full)).get("cpu_baseline", {})
+        ref32 = dict(value=rec.get("value"), cores=rec.get("cores"), source=os.path.relpath(full, HERE),
+                     note="the full 32-prompt batched run, measured once (not in this run)")
     return dict(value=round(audio / dt, 4), unit="audio-s/s", cores=threads, kind="port", cpu_model=cpu_model(),
-                affinity_cores=cores,
-                sample=f"{clips} clip(s) x {lcm_steps} LCM steps, {audio / clips:.3f} s each, batch 1 per clip, "
-                       f"fp32 torch-CPU oracle; median of 3 timed runs after 1 warm-up "
-                       f"({', '.join(f'{t:.2f}' for t in times)} s)")
+                affinity_cores=cores, full_batch32_committed=ref32,
+                sample=f"{clips} prompts in one batched call ({lcm_steps} LCM steps, batched VAE decode + BigVGAN), "
+                       f"{audio / clips:.3f} s clips = {audio:.1f} audio-s; fp32 torch-CPU oracle on {threads} "
+                       f"threads; one timed run ({dt:.1f} s) after a batch-1 warm-up")
 
 
 def pmc_traffic(kernel: str):
@@ -155,25 +196,27 @@ def extra_configs(pipe, a):
 def main():
     a = parse()
     from audiolcm_amd import _hip, recipe
-    from audiolcm_amd.distributed import all_gather_rows, init_from_env
+    from audiolcm_amd.distributed import all_gather_rows, all_reduce_max, barrier, init_from_env
     from audiolcm_amd.pipeline import AudioLCMPipeline
     import torch.distributed as dist
 
     from audiolcm_amd import roofline as RL
     model_roof = RL.summary(RL.path_layers(B=a.batch, S=a.lcm_steps, T=a.latent_len))
-    rank, world, local = init_from_env()
-    torch.cuda.set_device(local)
-    _hip.require_device(local)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = int(a.device_map.split(",")[local]) if a.device_map else local
+    rank, world, local = init_from_env(a.dist_backend, device=dev)
+    _hip.require_device(dev)
     B, S, T = a.batch, a.lcm_steps, a.latent_len
     pipe = AudioLCMPipeline.from_recipe(0, split=a.mode)
     ids = list(range(rank * B, (rank + 1) * B))
     cond = torch.cat([recipe.synthetic_context(1, seed0=1000 + i) for i in ids], 0).cuda()
     clip_sec = T * 2 * HOP / SR
 
+    gathered = {}
+
     def step():
         out = pipe.generate(cond, seeds=ids, steps=S, latent_len=T)
-        if world > 1:
-            all_gather_rows(out["wav"], B * world)
+        gathered["wav"] = all_gather_rows(out["wav"], B * world) if world > 1 else out["wav"]
         return out
 
     def timed(k, profile):
@@ -181,7 +224,7 @@ def main():
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            barrier()
         torch.cuda.synchronize()
         if profile:
             _hip.profile_begin()
@@ -190,18 +233,21 @@ def main():
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            barrier()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         prof = _hip.profile_end() if profile else []
         if world > 1:
-            t = torch.tensor([dt], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+            dt = all_reduce_max(dt)
         return dt, prof
 
     # headline: the production schedule (BigVGAN resblock chains on three streams), no per-launch events
+    log(f"rank {rank}/{world}: pipeline ready, headline pass ({a.warmup} warm-up + {a.steps} timed steps)")
     dt, _ = timed(a.steps, False)
+    log(f"headline {1e3 * dt / a.steps:.2f} ms/step; roofline pass")
+    if a.dump_wav and rank == 0:
+        import numpy as np
+        np.save(a.dump_wav, gathered["wav"].float().cpu().numpy())
     value = world * B * clip_sec * a.steps / dt
     # roofline pass: the same steps with live HIP-event timing of every launch and the resblock streams
     # serialised, so a kernel's measured duration is its own (concurrent kernels would share the chip)
@@ -236,6 +282,17 @@ def main():
                         measured_in=f"separate timed pass of the same {a.steps} steps, per-launch HIP events on the "
                                     f"launch streams, resblock streams serialised ({1e3 * dt_prof / a.steps:.2f} "
                                     f"ms/step)")
+        hb = sum(p["hbm_bytes"] for p in prof)
+        hms = sum(p["hbm_ms"] for p in prof)
+        if hms > 0:  # the HBM fraction of the HBM-bound subset of launches
+            roofline["hbm_subset"] = dict(
+                achieved=round(hb / (hms / 1e3) / 1e9, 1), peak=_hip.PEAK_HBM_BYTES / 1e9, unit="GB/s",
+                frac=round(hb / (hms / 1e3) / _hip.PEAK_HBM_BYTES, 4),
+                launches_per_step=round(sum(p["hbm_launches"] for p in prof) / a.steps, 1),
+                ms_per_step=round(hms / a.steps, 3), share_of_gpu_time=round(hms / max(gpu_ms, 1e-9), 4),
+                algorithmic_gb_per_step=round(hb / a.steps / 1e9, 3),
+                note="launches whose algorithmic flops/bytes < 2.5 PF / 8 TB/s: sum of algorithmic bytes / (sum of "
+                     "their event time x 8 TB/s)")
         tr = pmc_traffic(dom["name"])
         if tr:  # HBM bytes per launch from the committed PMC passes of this kernel
             roofline["traffic"] = tr["bytes_per_launch"]
@@ -251,8 +308,10 @@ def main():
                             parallelism=f"dp{world} (prompt shards, RCCL all-gather of waveforms)"),
                 roofline=roofline)
     if world == 1 and a.extra_configs:
+        log("other configs (C4, C5)")
         line["other_configs"] = extra_configs(pipe, a)
     if world == 1 and a.also_other_mode:
+        log("other precision policies")
         for other in ("mixed", "split", "bf16"):
             if other == a.mode:
                 continue
@@ -272,7 +331,7 @@ def main():
                       f"roof {p['roof_ms'] / a.steps:7.3f}", file=sys.stderr)
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
 
 

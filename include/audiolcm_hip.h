@@ -317,6 +317,10 @@ typedef struct alcm_prof_entry {
   double flops;
   double bytes;
   double roof_ms; /* sum over launches of max(flops/peak_flops, bytes/peak_bw) */
+  /* the HBM-bound launches of this entry (algorithmic flops/bytes below peak_flops/peak_bw) */
+  int64_t hbm_launches;
+  double hbm_ms;
+  double hbm_bytes;
 } alcm_prof_entry;
 int alcm_profile_begin(double peak_flops, double peak_bytes_per_s);
 int alcm_profile_end(alcm_prof_entry* out, int max_entries, int* n_entries);

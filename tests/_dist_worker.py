@@ -2,7 +2,7 @@
 import torch
 import torch.distributed as dist
 
-from audiolcm_amd.distributed import all_gather_rows, generate_sharded, init_from_env, shard_range
+from audiolcm_amd.distributed import all_reduce_max, barrier, generate_sharded, init_from_env, shard_range
 
 
 def main():
@@ -18,7 +18,8 @@ def main():
     assert torch.equal(full, expect), (rank, full)
     lo, hi = shard_range(n, rank, world)
     assert hi - lo == (3 if rank == 0 else 2)
-    dist.barrier()
+    assert all_reduce_max(0.5 + rank) == 0.5 + world - 1  # bench.py's max-over-ranks timing
+    barrier()
     if rank == 0:
         print("GATHER_OK")
     dist.destroy_process_group()

@@ -1,0 +1,52 @@
+"""bench.py's N>1 branch (BASELINE configs[2] / SURVEY §8e) executed on the leased GPU at world 2.
+
+Two torchrun ranks share GPU 0 (``--device-map 0,0``; RCCL refuses two ranks on one device, so the group is gloo
+and the waveform all-gather goes through the host — the code path is otherwise bench.py's own: env
+rendezvous, per-rank device, barrier + synchronize around the timed steps, max-over-ranks timing, contiguous
+prompt shards, all_gather_rows).  The gathered (2 x 32, 159744) waveforms must be bit-identical to one process
+generating the same 64 prompt ids (per-prompt seeds make every clip shard-invariant; 32 prompts per rank keeps
+every layer on the same kernel variant as the 64-prompt batch).  Reference sharding:
+ldm/data/joinaudiodataset_anylen.py:165.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+ARGS = ["--steps", "1", "--warmup", "0", "--also-other-mode", "0", "--cpu-baseline", "0", "--extra-configs", "0"]
+
+
+def _run(cmd, tmp_path, name):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=REPO)
+    with open(tmp_path / f"{name}.log", "w") as log:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=log, text=True, timeout=420, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + open(tmp_path / f"{name}.log").read()[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_world2_gathers_bit_identical_waveforms(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    bench = os.path.join(REPO, "bench.py")
+    one = _run([sys.executable, bench, "--gpus", "1", "--batch", "64", "--dump-wav", str(tmp_path / "w1.npy")]
+               + ARGS, tmp_path, "world1")
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                "--master-addr=127.0.0.1", "--master-port=29583", bench, "--gpus", "2", "--batch", "32",
+                "--dist-backend", "gloo", "--device-map", "0,0", "--dump-wav", str(tmp_path / "w2.npy")] + ARGS,
+               tmp_path, "world2")
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 64 and one["config"]["global_batch"] == 64
+    assert two["value"] > 0 and two["ms_per_step"] > 0
+    w1, w2 = np.load(tmp_path / "w1.npy"), np.load(tmp_path / "w2.npy")
+    assert w1.shape == w2.shape == (64, 159744)
+    assert np.isfinite(w1).all() and np.abs(w1).max() > 0
+    assert np.array_equal(w1, w2)
