@@ -20,6 +20,8 @@ static Knobs read_knobs() {
   k.wconv = env_int("ALCM_WCONV", 8);
   k.wconv_ablate = env_int("ALCM_WCONV_ABLATE", 0);
   k.wconv_order = env_int("ALCM_WCONV_ORDER", -1);
+  k.wconv_tile = env_int("ALCM_WCONV_TILE", -1);
+  k.wconv_fpipe = env_int("ALCM_WCONV_FPIPE", 1);
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;

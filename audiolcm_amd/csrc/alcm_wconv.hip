@@ -48,6 +48,7 @@ struct WConvDev {
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
+  int fpipe;            // wconv2: fragment-pipelined K loop (ALCM_WCONV_FPIPE)
   int ablate;           // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue,
                         // 2 no MFMA, 4 no global -> LDS staging in the K loop
 };
@@ -361,31 +362,41 @@ __global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Two-workgroups-per-CU variant (ALCM_WCONV=8): tile 128 rows x 192 columns, 4 waves as 2 (M) x 2 (N), each
-// wave 64 x 96 (4 x 6 16x16x32 MFMAs per 32-deep K slice, 0.42 fragment reads per MFMA).  72 KB of LDS
-// (one input window of <= 192 rows x 64 channels + two weight tiles) so two workgroups share a CU: the
-// HBM-bound epilogue (fp32 output + residual + accumulate) of one overlaps the MFMA K loop of the other,
-// where the 256-row kernel above serialises them (its epilogue is 26-80 % of its time on the BigVGAN shapes,
-// scripts/microbench.py wablate).  K steps: weights double-buffered (step s+1 staged while step s computes,
-// vmcnt(0) + barrier per step); the window is single-buffered and re-staged at each 64-channel chunk
+// Two-workgroups-per-CU variant (ALCM_WCONV=8): 4 waves, each 64 rows x 96 columns (4 x 6 16x16x32 MFMAs per
+// 32-deep K slice, 0.42 fragment reads per MFMA), tile BM x BN = 128 x 192 (waves 2 (M) x 2 (N)) or 256 x 96
+// (waves 4 (M) x 1 (N)).  <= 72 KB of LDS (one input window of BM + 64 rows x 64 channels + two weight tiles) so
+// two workgroups share a CU: the HBM-bound epilogue (fp32 output + residual + accumulate) of one overlaps the MFMA
+// K loop of the other, where the 256-row kernel above serialises them (its epilogue is 26-80 % of its time on the
+// BigVGAN shapes, scripts/microbench.py wablate).  K steps: weights double-buffered (step s+1 staged while step s
+// computes, vmcnt(0) + barrier per step); the window is single-buffered and re-staged at each 64-channel chunk
 // boundary (the stall is covered by the other workgroup).
-constexpr int W2_BM = 128, W2_BN = 192, W2_WROWS = 192;
+//
+// Tile choice: every tile re-reads the whole weight slice of its N columns once per M tile, so the L2 -> LDS
+// bytes per MFMA flop are ~ 1 / BM for the weights and ~ 1 / (k BN) for the window.  At 128 x 192 the two
+// co-resident workgroups of a CU fetch ~32 B/cycle at full MFMA rate on the k = 7 / 11 / 9 shapes, the per-CU
+// L2 -> LDS rate measured in MI355X_MICROARCH.md ("Indexed rows"), which is what the DMA ablation shows; 256 x 96
+// halves the weight bytes (and doubles the window bytes, amortised over k taps).
+constexpr int W2_HALO = 64;  // max (k - 1) * dil
 
-// ACT (ALCM_WIDE_ACT_FUSION): fused Activation1d epilogue (alcm_actepi.h) — tiles of 128 conv rows emit the middle
-// 112 (tstride 112, tshift 8), v = conv + bias (+ res) staged per 96-column half in LDS, fp32 out for owned rows,
-// Activation1d of owned rows written into the next conv's operand planes
-template <int PREC, bool GEGLU, int AB = 0, bool ACT = false>
+// ACT (ALCM_WIDE_ACT_FUSION, 128 x 192 only): fused Activation1d epilogue (alcm_actepi.h) — tiles of 128 conv rows
+// emit the middle 112 (tstride 112, tshift 8), v = conv + bias (+ res) staged per 96-column half in LDS, fp32 out
+// for owned rows, Activation1d of owned rows written into the next conv's operand planes
+template <int PREC, bool GEGLU, int AB = 0, bool ACT = false, int BM = 128, int BN = 192>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
-  constexpr int WBUF = W2_WROWS * 128;   // window image (24 KB)
-  constexpr int BBUF = W2_BN * 128;      // weight image (24 KB)
-  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB
-  constexpr int WPW = W2_WROWS / 8 / 4;  // window DMA instructions per wave (6)
-  constexpr int BPW = W2_BN / 8 / 4;     // weight DMA instructions per wave per step (6)
+  constexpr int WGM = BM / 64, WGN = 4 / WGM;   // wave grid
+  static_assert(WGM * WGN == 4 && WGN * TN * 16 == BN, "4 waves of 64 x 96");
+  static_assert(!ACT || (BM == 128 && BN == 192), "the fused activation epilogue is built for 128 x 192 tiles");
+  constexpr int WROWS = BM + W2_HALO;
+  constexpr int WBUF = WROWS * 128;      // window image
+  constexpr int BBUF = BN * 128;         // weight image
+  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB (128 x 192) / 64 KB (256 x 96)
+  constexpr int WPW = WROWS / 8 / 4;     // window DMA instructions per wave (6 / 10)
+  constexpr int BPW = BN / 8 / 4;        // weight DMA instructions per wave per step (6 / 3)
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q = P.nwg >> 3, r8 = P.nwg & 7;
   const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
@@ -400,9 +411,9 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   }
   const int b = mt / P.tiles_per_batch;
   const int t0 = (mt - b * P.tiles_per_batch) * P.tstride - P.tshift;
-  const int col0 = nt * W2_BN;
+  const int col0 = nt * BN;
   const int K = P.ksize, Cp = P.Cp;
-  const int WR = W2_BM + (K - 1) * P.dil;
+  const int WR = BM + (K - 1) * P.dil;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -452,46 +463,122 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     stage_w(0);
     stage_b(0, 0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    int st = 0;
-    for (int c = 0; c < nC; ++c) {
-      for (int tap = 0; tap < K; ++tap, ++st) {
-        if (st + 1 < steps && !no_dma && !no_wdma) stage_b(st + 1, (st + 1) & 1);
-        const char* Bl = smem + WBUF + (st & 1) * BBUF;
+    if (P.fpipe && !no_mfma && !no_sync) {
+      // fragment-pipelined K loop (ALCM_WCONV_FPIPE, default): the second 32-deep slice's fragments are read
+      // while the first slice's MFMAs run (B fragments as their last use retires, A fragments after each row),
+      // and the next step's A fragments (same chunk: the window is resident) during the second slice, so after
+      // each step's barrier only the 6 weight-fragment reads of the new step are exposed, not 10 reads per slice
+      auto rdA = [&](int tap, int sub, int i) -> bf16x8 {
         const int arow = arow0 + tap * P.dil;
-        const int asw = arow & 7;
+        return *reinterpret_cast<const bf16x8*>(smem + arow * 128 + (((4 * sub + (lane >> 4)) ^ (arow & 7)) << 4) +
+                                                i * 16 * 128);
+      };
+      auto rdB = [&](const char* Bl, int sub, int j) -> bf16x8 {
+        return *reinterpret_cast<const bf16x8*>(Bl + nrow0 * 128 + (((4 * sub + (lane >> 4)) ^ bsw) << 4) +
+                                                j * 16 * 128);
+      };
+      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const int ls = 4 * sub + (lane >> 4);
-          bf16x8 af[TM], bfr[TN];
-          const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
+      for (int i = 0; i < TM; ++i) af[i] = rdA(0, 0, i);
+      int st = 0;
+      for (int c = 0; c < nC; ++c) {
+        for (int tap = 0; tap < K; ++tap, ++st) {
+          if (st + 1 < steps && !no_dma) stage_b(st + 1, (st + 1) & 1);
+          const char* Bl = smem + WBUF + (st & 1) * BBUF;
 #pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
-          const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
+          for (int j = 0; j < TN; ++j) bfr[j] = rdB(Bl, 0, j);
+          __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
-          if constexpr (no_mfma) {
+          for (int i = 0; i < TM; ++i) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+              if (i == TM - 1) bfr[j] = rdB(Bl, 1, j);
+            }
+            af[i] = rdA(tap, 1, i);
+          }
+          // the next step's A fragments: tap + 1 of this chunk (at the chunk's last tap a harmless re-read of this
+          // window, replaced after the re-stage below)
+          const int ntap = tap + 1 < K ? tap + 1 : tap;
 #pragma unroll
-              for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][1];
-          } else {
-            // raised priority while this wave issues its MFMA block, so the co-resident workgroup's waves (in their
-            // staging / epilogue phases) do not interleave VALU work into it (-2..-5 % on the k11 shapes)
-            __builtin_amdgcn_s_setprio(1);
+          for (int i = 0; i < TM; ++i) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+            af[i] = rdA(ntap, 0, i);
+          }
+          // pin that interleave (hipcc otherwise sinks the reads behind the slice's MFMAs to save registers):
+          // masks MFMA = 0x8, DS_READ = 0x100
 #pragma unroll
-              for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
-            __builtin_amdgcn_s_setprio(0);
+          for (int i = 0; i < TM - 1; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_s_setprio(0);
+          if (tap == K - 1 && c + 1 < nC) {
+            // every wave has finished reading window c: re-stage it with chunk c + 1
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (!no_dma) stage_w(c + 1);
+          }
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (tap == K - 1) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = rdA(0, 0, i);
           }
         }
-        if constexpr (no_sync) continue;
-        if (tap == K - 1 && c + 1 < nC && !no_win) {
-          // every wave has finished reading window c: re-stage it with chunk c + 1
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          if (!no_dma) stage_w(c + 1);
+      }
+    } else {
+      int st = 0;
+      for (int c = 0; c < nC; ++c) {
+        for (int tap = 0; tap < K; ++tap, ++st) {
+          if (st + 1 < steps && !no_dma && !no_wdma) stage_b(st + 1, (st + 1) & 1);
+          const char* Bl = smem + WBUF + (st & 1) * BBUF;
+          const int arow = arow0 + tap * P.dil;
+          const int asw = arow & 7;
+#pragma unroll
+          for (int sub = 0; sub < 2; ++sub) {
+            const int ls = 4 * sub + (lane >> 4);
+            bf16x8 af[TM], bfr[TN];
+            const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
+            const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
+            if constexpr (no_mfma) {
+#pragma unroll
+              for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][1];
+            } else {
+              // raised priority while this wave issues its MFMA block, so the co-resident workgroup's waves (in their
+              // staging / epilogue phases) do not interleave VALU work into it (-2..-5 % on the k11 shapes)
+              __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+              for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
+              __builtin_amdgcn_s_setprio(0);
+            }
+          }
+          if constexpr (no_sync) continue;
+          if (tap == K - 1 && c + 1 < nC && !no_win) {
+            // every wave has finished reading window c: re-stage it with chunk c + 1
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (!no_dma) stage_w(c + 1);
+          }
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
     }
     if constexpr (no_sync) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -508,7 +595,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   }
 
   if constexpr (ACT) {
-    constexpr int HC = W2_BN / 2;  // the 96 columns of the waves with wn == h
+    constexpr int HC = BN / 2;  // the 96 columns of the waves with wn == h
     constexpr int AOTS = HC + 4;
     constexpr int acq = HC / 4;
     float* aot = reinterpret_cast<float*>(smem);  // 128 x 100 floats (51 KB): the K loop's last barrier retired it
@@ -528,7 +615,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       }
       __syncthreads();
       if (P.res || P.out) {
-        for (int e = tid; e < W2_BM * acq; e += 256) {
+        for (int e = tid; e < BM * acq; e += 256) {
           const int m = e / acq, n = (e - m * acq) * 4;
           const int t = t0 + m;
           if (t < 0 || t >= P.T) continue;
@@ -557,13 +644,13 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     return;
   }
 
-  // epilogue: one 64-row half of the tile at a time through LDS (the K loop's last barrier retired every
-  // fragment read and DMA), whole 768-B row segments with 16-B loads / stores
-  constexpr int OTS = W2_BN + 4;
+  // epilogue: one 64-row slice of the tile at a time through LDS (the K loop's last barrier retired every
+  // fragment read and DMA), whole row segments (768 / 384 B) with 16-B loads / stores
+  constexpr int OTS = BN + 4;
   float* ot = reinterpret_cast<float*>(smem);
-  constexpr int cq = W2_BN / 4;
-  constexpr int PER = 64 * cq / 256;  // float4 per thread per half (12)
-  for (int h = 0; h < 2; ++h) {
+  constexpr int cq = BN / 4;
+  constexpr int PER = 64 * cq / 256;  // float4 per thread per slice (12 / 6)
+  for (int h = 0; h < WGM; ++h) {
     if (wm == h) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -629,6 +716,15 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   }
 }
 
+// wconv2 tile by shape (ALCM_WCONV_TILE = -1): 256 x 96 where the weight stream dominates the per-CU fetch (k >= 7:
+// the window is amortised over >= 7 taps) and there is at least one 256-row tile per CU; 128 x 192 elsewhere.
+// Measured per launch (B = 32, scripts/microbench.py wablate, one box): s0 C768 k11 0.946 -> 0.860 ms, s1 C384 k11
+// 0.973 -> 0.934, s2 C192 k11 0.583 -> 0.559, DiT FFN-down 0.377 -> 0.358; k3 shapes equal or slower (VAE k3 +17 %)
+static bool wconv2_tile256(const alcm_opconv_args& a) {
+  const int64_t mt = (int64_t)a.B * ((a.T + 255) / 256);
+  return a.out_stride <= 0 && a.ksize >= 7 && mt * (a.N / 96) >= 256;
+}
+
 // Eligible: single-plane precisions, N a multiple of 128, Cp a multiple of 64, 2 <= k, (k-1)d <= 64,
 // no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
@@ -645,7 +741,11 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
-  if ((var == 8 || strided) && !(act && strided) && a.N % W2_BN == 0 && (a.ksize - 1) * a.dil <= W2_WROWS - W2_BM) {
+  // wconv2 tile (ALCM_WCONV_TILE): 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
+  const int tk = knobs().wconv_tile;
+  const bool t256 = !act && a.N % 96 == 0 && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
+  const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
+  if ((var == 8 || strided) && !(act && strided) && a.N % BN2 == 0 && (a.ksize - 1) * a.dil <= W2_HALO) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
@@ -656,8 +756,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;
     P.ablate = act ? 0 : knobs().wconv_ablate;
+    P.fpipe = knobs().wconv_fpipe;
     // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 128 conv rows and emits the middle 112
-    P.tstride = act ? W2_BM - 2 * ACT_EPI_HALO : W2_BM;
+    P.tstride = act ? BM2 - 2 * ACT_EPI_HALO : BM2;
     P.tshift = act ? ACT_EPI_HALO : 0;
     if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
     // N-tile-major order where the weight matrix is long (Cp * k >= 4096) and there are enough M tiles to share
@@ -667,40 +768,43 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     const int ord = knobs().wconv_order;
     P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && tiles_m >= 128);
     P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
-    P.tiles_n = a.N / W2_BN;
+    P.tiles_n = a.N / BN2;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
     if (nwg2 >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
     P.nwg = (int)nwg2;
     void* tok = prof_start(s);
     const dim3 grid((unsigned)nwg2), blk(256);
     const bool gl = a.geglu_plane != nullptr;
+    auto go = [&](auto bm_c) {
+      constexpr int BM = decltype(bm_c)::value, BN = BM == 256 ? 96 : 192;
+      if (a.prec == PREC_F16 && !gl && P.ablate) {
+        switch (P.ablate) {
+          case 1: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 1, false, BM, BN>), grid, blk, 0, s, P); break;
+          case 2: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 2, false, BM, BN>), grid, blk, 0, s, P); break;
+          case 4: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 4, false, BM, BN>), grid, blk, 0, s, P); break;
+          default: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 5, false, BM, BN>), grid, blk, 0, s, P); break;
+        }
+      } else if (a.prec == PREC_F16) {
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true, 0, false, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 0, false, BM, BN>), grid, blk, 0, s, P);
+      } else {
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true, 0, false, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, 0, false, BM, BN>), grid, blk, 0, s, P);
+      }
+    };
     if (act) {
       if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 0, true>), grid, blk, 0, s, P);
       else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, 0, true>), grid, blk, 0, s, P);
-    } else if (a.prec == PREC_F16 && !gl && P.ablate) {
-      switch (P.ablate) {
-        case 1: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 1>), grid, blk, 0, s, P); break;
-        case 2: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 2>), grid, blk, 0, s, P); break;
-        case 4: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 4>), grid, blk, 0, s, P); break;
-        case 6: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 6>), grid, blk, 0, s, P); break;
-        case 8: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 8>), grid, blk, 0, s, P); break;
-        case 16: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 16>), grid, blk, 0, s, P); break;
-        case 17: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 17>), grid, blk, 0, s, P); break;
-        case 32: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 32>), grid, blk, 0, s, P); break;
-        default: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 3>), grid, blk, 0, s, P); break;
-      }
-    } else if (a.prec == PREC_F16) {
-      if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true>), grid, blk, 0, s, P);
-      else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false>), grid, blk, 0, s, P);
+    } else if (t256) {
+      go(std::integral_constant<int, 256>{});
     } else {
-      if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true>), grid, blk, 0, s, P);
-      else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false>), grid, blk, 0, s, P);
+      go(std::integral_constant<int, 128>{});
     }
     if (tok) {
-      char name[96];
+      char name[112];
       // the demangled rocprofv3 name (template defaults included), so bench.py can join the PMC passes by name
-      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s, 0, %s>", a.prec, gl ? "true" : "false",
-                    act ? "true" : "false");
+      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s, 0, %s, %d, %d>", a.prec, gl ? "true" : "false",
+                    act ? "true" : "false", BM2, BN2);
       if (knobs().prof_shapes)
         std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp,
                       a.N, a.ksize);

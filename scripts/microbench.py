@@ -178,11 +178,10 @@ def bench_wablate(B=32):
         pl = K.operand_planes(x, 2)
         tf = 2 * B * T * Cin * N * k / 1e12
         line, outs = [], []
-        for wco in [f"{w}/{o}" for w in os.environ.get("WCONV_VARS", "5").split(",")
-                    for o in os.environ.get("ORDERS", "0").split(",")]:
-            wc, order = wco.split("/")
-            os.environ["ALCM_WCONV"] = wc
-            os.environ["ALCM_WCONV_ORDER"] = order
+        # variants: KNOBS="ALCM_WCONV_TILE=0+ALCM_WCONV_FPIPE=0,ALCM_WCONV_TILE=1" (one ALCM_* assignment set each)
+        for var in os.environ.get("KNOBS", "ALCM_WCONV=8").split(","):
+            kv = dict(x.split("=") for x in var.split("+"))
+            os.environ.update(kv)
             for ab in os.environ.get("ABLATE", "0,1,2,4,6,3").split(","):
                 os.environ["ALCM_WCONV_ABLATE"] = ab
                 _hip.reload_knobs()
@@ -197,10 +196,10 @@ def bench_wablate(B=32):
                     y = fn()
                     yy = y if y is not None else o
                     outs.append((yy.view(torch.float16) if yy.dtype == torch.int16 else yy).float().clone())
-                line.append(f"w{wc}o{order}ab{ab} {ms:7.3f}")
+                line.append(f"{'/'.join(v for v in kv.values())}ab{ab} {ms:7.3f}")
+            for k in kv:
+                os.environ.pop(k)
         os.environ.pop("ALCM_WCONV_ABLATE")
-        os.environ.pop("ALCM_WCONV_ORDER")
-        os.environ.pop("ALCM_WCONV")
         _hip.reload_knobs()
         ms0 = float(line[0].split()[1])
         diff = max([float((outs[0] - x).abs().max()) for x in outs[1:]] or [0.0])
