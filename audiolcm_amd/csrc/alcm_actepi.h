@@ -169,4 +169,40 @@ __device__ __forceinline__ void act_epilogue_tile(const float* tile, int ots, in
   }
 }
 
+// act_epilogue_tile with the channel pairs NP of the tile known at compile time and no operand-padding work (the
+// caller's planes keep their padding channels, which no consumer reads): work item w = (run, pair) by a constant
+// division, the caller picks R so that NP * runs ~ its thread count (one pass)
+template <int PREC, int R, int NP>
+__device__ __forceinline__ void act_epilogue_ct(const float* tile, int ots, int trow0, int e_lo, int e_hi, int T,
+                                                int c0, int b, const ActEpiDev& A, int tid, int nthr) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  const int nrun = (e_hi - e_lo + R - 1) / R;
+  for (int w = tid; w < NP * nrun; w += nthr) {
+    const int run = w / NP, p = w - run * NP;
+    const int c = c0 + 2 * p;
+    const int j0 = e_lo + run * R;
+    const int jn = min(R, e_hi - j0);
+    u16* yb = A.plane + ((int64_t)b * T) * A.Cp + c;
+    const float* col = tile + 2 * p;
+    const f32x2 ear = f32x2{A.aexp[c], A.aexp[c + 1]} * INV_PI;
+    const f32x2 h = f32x2{A.ibeta[c], A.ibeta[c + 1]} * 0.5f;
+    if (jn == R && j0 >= 6 && j0 + R + 6 <= T) {
+      f32x2 win[R + 12];
+#pragma unroll
+      for (int i = 0; i < R + 12; ++i) win[i] = *reinterpret_cast<const f32x2*>(col + (j0 - 6 + i - trow0) * ots);
+      f32x2 o[R];
+      act_run_interior<R>(win, A.f, ear, h, o);
+#pragma unroll
+      for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o[r]);
+    } else {
+      for (int r = 0; r < jn; ++r) {
+        const f32x2 o = act_one_clamped(j0 + r, T, A.f, ear, h, [&](int i) {
+          return *reinterpret_cast<const f32x2*>(col + (i - trow0) * ots);
+        });
+        op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o);
+      }
+    }
+  }
+}
+
 }  // namespace alcm

@@ -61,6 +61,12 @@ bool opconv_act_supported(int prec, int N, int Cp_in);
 int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s);
 
+// narrow AMPBlock conv with resident dense weights (alcm_tconv.hip); actepi: const ActEpiDev* or nullptr
+bool tconv_supported(int prec, int C, int N, int ksize, int dil);
+struct ActEpiDev;
+int tconv(const alcm_opconv_args& a, const unsigned short* wd, int64_t wd_lo, int kd, const ActEpiDev* act,
+          double flops, double bytes, hipStream_t s);
+
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
   int wconv = 8;                 // ALCM_WCONV: 8 = 2-workgroup/CU kernel, 5 = 256-row kernel, 0 = neither
@@ -85,6 +91,11 @@ struct Knobs {
   bool tail_f16w2_all = false;   // ALCM_TAIL_F16W2_ALL
   bool serial_resblocks = false; // ALCM_SERIAL_RESBLOCKS: default of alcm_model_set_resblock_streams
   bool prof_shapes = false;      // ALCM_PROF_SHAPES: split profile rows per layer shape
+  int opconv_ablate = 0;         // ALCM_OPCONV_ABLATE: timing-only ablation bits of opconv_kernel (1 no epilogue,
+                                 // 2 no MFMA)
+  int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
+                                 // 2 no MFMA, 4 no window DMA)
+  int tconv = 1;                 // ALCM_TCONV: resident-weight narrow conv for BigVGAN stages 3-5 (0 = opconv / nconv)
   int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
 };
 const Knobs& knobs();

@@ -40,6 +40,9 @@ static Knobs read_knobs() {
   k.serial_resblocks = env_set("ALCM_SERIAL_RESBLOCKS");
   k.prof_shapes = env_set("ALCM_PROF_SHAPES");
   k.tail_prefetch = env_int("ALCM_TAIL_PREFETCH", 1);
+  k.opconv_ablate = env_int("ALCM_OPCONV_ABLATE", 0);
+  k.tconv = env_int("ALCM_TCONV", 1);
+  k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   return k;
 }
 

@@ -17,6 +17,7 @@
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
+#include "alcm_actepi.h"
 
 namespace alcm {
 
@@ -51,6 +52,7 @@ struct Packed {
 };
 struct ConvW {
   Packed w;
+  Packed dw;  // BigVGAN narrow stages: dense K = tap * C + c packing for the resident-weight conv (alcm_tconv.hip)
   float* b = nullptr;
 };
 struct NormW {
@@ -574,7 +576,9 @@ static void build_voc(Ingest& I, const int* ic, int nic) {
           const std::string cp = rp + (which ? "convs2." : "convs1.") + std::to_string(l) + ".";
           ConvW cw;
           // K = tap*Cp + ci with Cp = round_up(C, 32): the layout of the operand planes alcm_opconv reads
-          cw.w = I.pack(I.wn(cp, {S.cout, S.cout, A.k}), S.cout, S.cout, A.k, 0, 1, 0, 32);
+          const std::vector<float> wv = I.wn(cp, {S.cout, S.cout, A.k});
+          cw.w = I.pack(wv, S.cout, S.cout, A.k, 0, 1, 0, 32);
+          if (S.cout <= 96 && S.cout % 8 == 0) cw.dw = I.pack(wv, S.cout, S.cout, A.k, 0, 1, 0, 8);
           cw.b = I.upload(I.get(cp + "bias", {S.cout}));
           (which ? A.c2 : A.c1).push_back(cw);
         }
@@ -1273,11 +1277,46 @@ static const alcm_model::AuxSet* voc_streams(alcm_model* m, hipStream_t s) {
 
 // conv on the operand planes `in`; with `act` the epilogue also writes Activation1d(conv + bias (+ res)) into
 // the planes `act_out` (alcm_actepi.h), and `out` may be null
+// the narrow stages' AMPBlock convs on the resident-weight kernel (alcm_tconv.hip): every conv of the stage or none
+// (its planes keep stale operand-padding channels, which only that kernel ignores)
+static bool stage_tconv(const StageW& S, int prec) {
+  if (S.rb.empty() || !S.rb[0].c1[0].dw.p) return false;
+  for (const AmpW& A : S.rb)
+    for (size_t l = 0; l < A.dil.size(); ++l)
+      if (!tconv_supported(prec, S.cout, S.cout, A.k, A.dil[l])) return false;
+  return true;
+}
+
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
                       float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
-                      const ActW* act = nullptr, u16* act_out = nullptr) {
+                      const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false) {
   alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
+  if (dense) {
+    g.a = in ? in : w.pl;
+    g.B = B; g.T = T; g.C = cw.w.cin; g.Cp = cw.w.cpad;
+    g.ksize = cw.w.taps; g.dil = dil; g.pad = (cw.w.taps - 1) * dil / 2;
+    g.N = cw.w.rows; g.bias = cw.b; g.res = res; g.out = out; g.out_scale = out_scale; g.accumulate = accumulate;
+    g.prec = prec;
+    ActEpiDev E{};
+    if (act) {
+      E.plane = act_out;
+      E.plane_lo = 0;
+      E.Cp = round_up(cw.w.rows, 32);
+      E.aexp = act->aexp;
+      E.ibeta = act->ibeta;
+      for (int k = 0; k < 12; ++k) {
+        E.f.up[k] = 2.0f * act->fup[k];
+        E.f.dn[k] = act->fdn[k];
+      }
+    }
+    const double M = (double)B * T;
+    const double flops = 2.0 * M * g.N * (double)g.ksize * g.C;
+    const double bytes = M * g.C * 2.0 + (double)g.N * cw.dw.kpad * 2.0 * (prec == PREC_F16W2 ? 2 : 1) +
+                         M * g.N * 4.0 * ((out ? 1 : 0) + (res ? 1 : 0) + (accumulate ? 1 : 0)) +
+                         (act ? M * g.N * 2.0 : 0.0);
+    return tconv(g, cw.dw.p + 2 * cw.dw.lo, cw.dw.lo, cw.dw.kpad, act ? &E : nullptr, flops, bytes, s);
+  }
   g.a = in ? in : w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
   if (act) {
     g.act_plane = act_out;
@@ -1359,6 +1398,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // writes the fp32 running state, ping-ponged between rb and y since its tiles overlap, plus planes)
     const float inv = 1.0f / (float)S.rb.size();
     const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
+    const bool dense = fuse && stage_tconv(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
     if (conc) {  // chains start after the upsampler wrote u
@@ -1378,12 +1418,13 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
         if (fuse) {
           if (l == 0) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
-                              &A.act[2 * l + 1], cb.pl2));
+                              &A.act[2 * l + 1], cb.pl2, dense));
           if (last) {
-            ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, x, inv, j > 0, 0, pamp, cb.pl2));
+            ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, x, inv, j > 0, 0, pamp, cb.pl2, nullptr, nullptr,
+                                dense));
           } else {
             ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, nxt, 1.f, 0, 0, pamp, cb.pl2, &A.act[2 * l + 2],
-                                cb.pl));
+                                cb.pl, dense));
             cur = nxt;
             nxt = nxt == cb.rb ? cb.t : cb.rb;
           }

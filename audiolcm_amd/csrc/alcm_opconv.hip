@@ -165,6 +165,7 @@ struct OpConvDev {
   int tstride, tshift;  // tile i of a batch computes rows [i * tstride - tshift, + BM)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
   int act_prefetch;     // ACT: residual prefetched into registers before the K loop
+  int ablate;           // diagnostics (ALCM_OPCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA
   int ostride, ooff, orows;  // output row of conv row t: b * orows + t * ostride + ooff (a ConvTranspose phase)
 };
 
@@ -368,6 +369,13 @@ __global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvD
       bh[j] = *reinterpret_cast<const bf16x8*>(bh_base + b_off + j * 16 * 32);
       if (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bl_base + b_off + j * 16 * 32);
     }
+    if (P.ablate & 2) {  // keep the fragment reads, skip the products
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(ah[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[j]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -412,6 +420,15 @@ __global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvD
     if (g < SPC) step(cc, g, more, S0{});
   }
 
+  if (P.ablate & 1) {
+    float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 123.f && P.out) P.out[tid] = sum;
+    return;
+  }
   // epilogue
   if constexpr (ACT) {
     // v = conv + bias (+ res) for every tile row inside [0, T) -> LDS; fp32 out (if any) for the rows this
@@ -675,6 +692,7 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
   P.act_prefetch = knobs().tail_prefetch;
+  P.ablate = knobs().opconv_ablate;
   P.ostride = strided ? a.out_stride : 1;
   P.ooff = strided ? a.out_offset : 0;
   P.orows = strided ? a.out_rows : a.T;

@@ -1,0 +1,371 @@
+// Narrow AMPBlock conv (BigVGAN stages 3-5, C = 96 / 48 / 24; vocoder/bigvgan/models.py:72-81) with the whole
+// weight matrix resident in LDS: a persistent workgroup loads its weights once and then walks output tiles, so
+// the K loop has no weight stream and no barriers.
+//
+// Why a separate kernel (scripts/microbench.py tailab / pmc_tail.sh on the stage-4 conv2 + residual + fused
+// Activation1d, opconv_kernel): 60k cycles per 256-row tile-wave, MFMA 22 % busy; half of it the fused
+// Activation1d epilogue (2.1k VALU instructions per wave, issued at the one-wave rate, items split 1.5 per thread
+// by runtime divisions, plus zero stores for the 48 -> 64 operand padding), half a K loop whose window and
+// weight tiles go through registers every 32-channel step (1.5k VALU instructions per wave, a barrier per step).
+//
+// Structure (one workgroup per CU, NW = BM / 32 waves, each 32 rows x NS columns):
+//   * K is dense: k = tap * C + c (no channel padding: 528 instead of 704 deep at C = 48, k = 11), rounded up to
+//     32; a lane's 8-element group never straddles a tap (C % 8 == 0), so its A fragment is one ds_read_b128 at
+//     window row (m + tap * d), column c;
+//   * weights [NSP][kd] fp16 (hi, and lo for the F16W2 precision) are DMA'd once per workgroup into rows of an
+//     odd number of 16-B slots (conflict-free ds_read_b128 of 16 consecutive rows), rows NS .. NSP-1 zero;
+//   * per tile: the input window (BM + (k-1)d rows x C channels, rows of an odd number of 16-B slots) by LDS-DMA,
+//     the residual rows into registers, then the barrier-free K loop; the epilogue stages v = conv + bias in LDS
+//     (over the dead window), adds the residual, writes the fp32 state rows it owns and applies Activation1d to
+//     them (act_epilogue_ct: compile-time channel pairs, one pass over the threads) into the next conv's planes;
+//   * C = 96 runs as two launches' worth of column halves (NS = 48 output channels per tile): its 96 x 1056
+//     weight matrix does not fit one CU's LDS.
+#include <cstdio>
+#include <cstring>
+
+#include "alcm_common.h"
+#include "alcm_internal.h"
+#include "alcm_actepi.h"
+
+namespace alcm {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __attribute__((aligned(16))) uint4 g_tconv_zero[8];  // a zero line for out-of-range DMA lanes
+
+struct TConvDev {
+  const u16* a;       // operand plane [B][T][Cp] (fp16); channels >= C are never read
+  int T, Cp, ksize, dil, pad;
+  const u16* w;       // dense fp16 weights [N][kd] (K = tap * C + c); lo plane at w + w_lo (F16W2)
+  int64_t w_lo;
+  int kd, N;
+  const float* bias;
+  const float* res;   // [B][T][N] or null
+  float* out;         // [B][T][N] or null
+  float out_scale;
+  int accumulate;
+  ActEpiDev act;      // act.plane == null: no Activation1d
+  int tiles_per_batch, ntiles, ncg;  // ncg: column groups (N / NS)
+  int wslots;         // 16-B slots per LDS weight row (odd)
+  int ablate;         // diagnostics (ALCM_TCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA,
+                      // 4 no window DMA
+};
+
+__device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
+}
+
+// C input channels, NS output channels per tile, NPB weight planes (1 = F16, 2 = F16W2), BM rows per tile,
+// R Activation1d rows per work item, WBYTES LDS bytes reserved for the weights (all planes)
+template <int C, int NS, int NPB, int BM, int R, int WBYTES, bool ACT, bool RES, bool OUTW, bool ACC>
+__global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
+  constexpr int NW = BM / 32, NT = NW * 64;
+  constexpr int TM = 2, NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
+  constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;  // window row: odd number of 16-B slots
+  constexpr int RS = RSS * 16;
+  constexpr int WRMAX = BM + 64;
+  constexpr int WIN_INSTR = (WRMAX * RSS + 63) / 64;    // window DMA instructions per tile (64 slots each)
+  constexpr int OTS = NS + 4;                           // staged fp32 row stride (floats)
+  constexpr int STAGE = BM * OTS * 4;
+  constexpr int WINB = WIN_INSTR * 1024;
+  constexpr int REGION = STAGE > WINB ? STAGE : WINB;   // window, then (after the K loop) the staged tile
+  constexpr int SMEM = WBYTES + REGION;
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(C % 8 == 0 && NS % 4 == 0, "geometry");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  char* const wl = smem;            // weights
+  char* const win = smem + WBYTES;  // window / staged tile
+  float* const ot = reinterpret_cast<float*>(win);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = P.ksize, dil = P.dil;
+  const int WS = P.wslots * 16;
+  const int nslice = P.kd / 32;
+
+  // ---- weights, once per workgroup: slot g of plane p -> row n = g / wslots, 16-B piece q = g % wslots
+  {
+    const int total = NSP * P.wslots;
+    const int instr = (total + 63) / 64;
+    for (int p = 0; p < NPB; ++p) {
+      for (int i = wave; i < instr; i += NW) {
+        const int g = i * 64 + lane;
+        const int n = g / P.wslots, q = g - n * P.wslots;
+        const bool ok = g < total && n < NS && q < P.kd / 8;
+        // column group of this workgroup's tiles is fixed: tiles are dealt so that ncg divides the stride
+        const int cg = blockIdx.x % P.ncg;
+        const u16* src = ok ? P.w + p * P.w_lo + (int64_t)(cg * NS + n) * P.kd + q * 8
+                            : reinterpret_cast<const u16*>(g_tconv_zero);
+        tc_glds16(src, wl + p * (WBYTES / NPB) + i * 1024);
+      }
+    }
+  }
+
+  const int wr0 = wave * 32;  // first tile row of this wave
+  const int q4 = lane >> 4, l16 = lane & 15;
+  constexpr int NRES = (BM * (NS / 4) + NT - 1) / NT;  // residual float4 per thread
+  const int cg = blockIdx.x % P.ncg;
+  const int n0 = cg * NS;
+  const int E = BM - 2 * ACT_EPI_HALO;  // emitted rows per tile
+  float bias_r[TN];                     // this lane's output-column biases, loaded once
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
+
+  for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
+    const int mt = tile / P.ncg;
+    const int b = mt / P.tiles_per_batch;
+    const int e0 = (mt - b * P.tiles_per_batch) * E;  // first emitted row
+    const int t0 = e0 - ACT_EPI_HALO;                 // first computed row
+    const int WR = BM + (K - 1) * dil;
+
+    // residual rows of the tile (clamped to [0, T)) into registers, ahead of the K loop
+    float4 rv[NRES];
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < NRES; ++i) {
+        const int e = tid + i * NT;
+        const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
+        const int t = min(max(t0 + m, 0), P.T - 1);
+        rv[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + t) * P.N + n0 + (e < BM * (NS / 4) ? n : 0));
+      }
+    }
+    // input window rows [t0 - pad, t0 - pad + WR): slot g -> row g / RSS, piece g % RSS (pieces >= C/8 zero)
+    for (int i = wave; i < WIN_INSTR && !(P.ablate & 4); i += NW) {
+      const int g = i * 64 + lane;
+      const int r = g / RSS, q = g - r * RSS;
+      const int ts = t0 - P.pad + r;
+      const bool ok = r < WR && q < C / 8 && ts >= 0 && ts < P.T;
+      const u16* src = ok ? P.a + ((int64_t)b * P.T + ts) * P.Cp + q * 8 : reinterpret_cast<const u16*>(g_tconv_zero);
+      tc_glds16(src, win + i * 1024);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- barrier-free K loop over 32-deep slices of the dense K
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* arow = win + (wr0 + l16) * RS;
+    const char* brow = wl + l16 * WS;
+    auto slice = [&](int s) {
+      const int kk = s * 32 + q4 * 8;
+      int tap = kk / C;
+      const int c = kk - tap * C;
+      tap = min(tap, K - 1);  // K padding: zero weights, any finite window value
+      bf16x8 af[TM], bh[TN], bl[NPB == 2 ? TN : 1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dil) * RS + c * 2);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(brow + j * 16 * WS + kk * 2);
+        if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(brow + WBYTES / 2 + j * 16 * WS + kk * 2);
+      }
+      if (P.ablate & 2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[j]));
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (NPB == 2) acc[i][j] = mfma16<PREC_F16>(af[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_F16>(af[i], bh[j], acc[i][j]);
+        }
+    };
+    // two slices per iteration: the second slice's fragment reads can issue under the first slice's MFMAs
+    int s = 0;
+    for (; s + 1 < nslice; s += 2) {
+      slice(s);
+      slice(s + 1);
+    }
+    if (s < nslice) slice(s);
+    __syncthreads();  // every window read retired: the region becomes the staged tile
+    if (P.ablate & 1) {
+      float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (sum == 123.f && P.out) P.out[tid] = sum;
+      continue;
+    }
+
+    // ---- epilogue: v = conv + bias -> LDS
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wr0 + i * 16 + q4 * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = j * 16 + l16;
+          if (n < NS) ot[m * OTS + n] = acc[i][j][r] + bias_r[j];
+        }
+      }
+    __syncthreads();
+    const int e_hi = min(e0 + E, P.T);
+    if constexpr (RES || OUTW || ACC) {
+      // + residual (all tile rows: the activation reads the halo rows too); fp32 state of the owned rows
+#pragma unroll
+      for (int i = 0; i < NRES; ++i) {
+        const int e = tid + i * NT;
+        if (e >= BM * (NS / 4)) break;
+        const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
+        const int t = t0 + m;
+        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+        if constexpr (RES) {
+          v.x += rv[i].x; v.y += rv[i].y; v.z += rv[i].z; v.w += rv[i].w;
+          if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+        }
+        if ((OUTW || ACC) && t >= e0 && t < e_hi) {
+          float* op = P.out + ((int64_t)b * P.T + t) * P.N + n0 + n;
+          if constexpr (ACC) {
+            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+            if (P.accumulate) {
+              const float4 pv = *reinterpret_cast<const float4*>(op);
+              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+            }
+          }
+          *reinterpret_cast<float4*>(op) = v;
+        }
+      }
+      if constexpr (ACT) __syncthreads();
+    }
+    if constexpr (ACT)
+      act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+    __syncthreads();  // staged-tile reads retired before the next window DMA overwrites the region
+  }
+}
+
+// -------------------------------------------------------------------------------------------------- host
+struct TConvCfg {
+  int C, NS, NPB, BM;
+};
+
+// weights bytes reserved per configuration (k <= 11): NSP rows x odd slots, rounded up to whole DMA instructions
+static constexpr int tc_wbytes(int C, int NS, int NPB) {
+  const int nsp = (NS + 15) / 16 * 16;
+  const int kd = (11 * C + 31) / 32 * 32;
+  const int slots = (kd / 8) % 2 ? kd / 8 : kd / 8 + 1;
+  return NPB * ((nsp * slots + 63) / 64) * 1024;
+}
+
+bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
+  if (knobs().tconv == 0) return false;
+  if (prec != PREC_F16 && prec != PREC_F16W2) return false;
+  if (C != N || ksize > 11 || (ksize - 1) * dil > 64) return false;
+  if (C == 96) return prec == PREC_F16;
+  return C == 48 || C == 24;
+}
+
+template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
+static void tc_launch(const TConvDev& P, int grid, hipStream_t s) {
+  constexpr int WB = tc_wbytes(C, NS, NPB);
+  hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, WB, ACT, RES, OUTW, ACC>), dim3(grid), dim3(BM * 2), 0, s, P);
+}
+
+template <int C, int NS, int NPB, int BM, int R>
+static int tc_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
+  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, true, false, false, false>(P, grid, s);
+  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, true, true, true, false>(P, grid, s);
+  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, false, true, false, true>(P, grid, s);
+  else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
+  return 0;
+}
+
+// conv on operand planes with dense fp16 weights `wd` ([N][kd], K = tap * C + c; lo plane wd_lo elements after
+// hi for F16W2): out / res fp32 [B][T][N], Activation1d of the result into act->plane (or none)
+int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const ActEpiDev* act, double flops,
+          double bytes, hipStream_t s) {
+  if (!tconv_supported(a.prec, a.C, a.N, a.ksize, a.dil)) return set_error(ALCM_E_INVALID, "tconv: unsupported shape");
+  if (kd != (a.ksize * a.C + 31) / 32 * 32 || !wd) return set_error(ALCM_E_INVALID, "tconv: dense weight layout");
+  if (2 * a.pad != (a.ksize - 1) * a.dil || a.out_stride > 0 || a.out_act || a.geglu_plane)
+    return set_error(ALCM_E_INVALID, "tconv: same-length convs only");
+  if ((((uintptr_t)a.a) & 15) || (((uintptr_t)wd) & 15) || (wd_lo % 8) || (a.Cp % 8) ||
+      (a.res && (((uintptr_t)a.res) & 15)) || (a.out && (((uintptr_t)a.out) & 15)))
+    return set_error(ALCM_E_INVALID, "tconv: alignment");
+  const bool acc_mode = !act && a.res && a.out;
+  if (act && (a.accumulate || (a.out && !a.res))) return set_error(ALCM_E_INVALID, "tconv: epilogue combination");
+  TConvDev P{};
+  P.a = (const u16*)a.a;
+  P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
+  P.w = wd; P.w_lo = wd_lo; P.kd = kd; P.N = a.N;
+  P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+  if (act) P.act = *act;
+  P.ablate = knobs().tconv_ablate;
+  const int slots = kd / 8;
+  P.wslots = slots % 2 ? slots : slots + 1;
+  const int npb = a.prec == PREC_F16W2 ? 2 : 1;
+  const int C = a.C;
+  const int BM = C == 96 ? 192 : 256;
+  const int NS = C == 96 ? 48 : C;
+  P.ncg = a.N / NS;
+  P.tiles_per_batch = (a.T + (BM - 2 * ACT_EPI_HALO) - 1) / (BM - 2 * ACT_EPI_HALO);
+  const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.ncg;
+  if (nt >= (1ll << 30)) return set_error(ALCM_E_INVALID, "tconv: problem too large");
+  P.ntiles = (int)nt;
+  // persistent: one workgroup per CU (the LDS holds the weights), a multiple of ncg so a workgroup's column group
+  // (blockIdx % ncg) is the same for every tile it takes (tile % ncg == blockIdx % ncg)
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  int grid = std::min<int64_t>(nt, (int64_t)ncu);
+  grid = std::max(P.ncg, grid / P.ncg * P.ncg);
+  const bool outw = a.out && !acc_mode;
+  void* tok = prof_start(s);
+  int rc;
+  if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);
+  else if (C == 48) {
+    if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+    else rc = tc_mode<48, 48, 1, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+  } else {
+    if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+    else rc = tc_mode<24, 24, 1, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+  }
+  if (rc) return rc;
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::tconv_kernel<C%d, W%d, %s%s%s>", C, npb, act ? "act" : "",
+                  a.res ? "+res" : "", acc_mode ? "+acc" : "");
+    if (knobs().prof_shapes)
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d k%d", a.T, a.ksize);
+    prof_stop(tok, s, name, flops, bytes);
+  }
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace alcm
+
+extern "C" int alcm_opconv_dense(const alcm_opconv_args* args, alcm_stream_t stream) {
+  using namespace alcm;
+  if (!args || !args->a || !args->w || args->B <= 0 || args->T <= 0) return set_error(ALCM_E_INVALID, "opconv_dense: bad arguments");
+  const alcm_opconv_args& a = *args;
+  ActEpiDev E{};
+  const bool act = a.act_plane != nullptr;
+  if (act) {
+    if (!a.act_alpha_exp || !a.act_inv_beta || !a.act_up_filter || !a.act_down_filter || a.N % 2)
+      return set_error(ALCM_E_INVALID, "opconv_dense: activation parameters");
+    E.plane = (u16*)a.act_plane;
+    E.plane_lo = 0;
+    E.Cp = round_up(a.N, 32);
+    E.aexp = a.act_alpha_exp;
+    E.ibeta = a.act_inv_beta;
+    for (int k = 0; k < 12; ++k) {
+      E.f.up[k] = 2.0f * a.act_up_filter[k];
+      E.f.dn[k] = a.act_down_filter[k];
+    }
+  }
+  const double M = (double)a.B * a.T;
+  const double flops = 2.0 * M * a.N * (double)a.ksize * a.C;
+  const double bytes = M * a.C * 2.0 + (double)a.N * a.kpad * 2.0 * (a.prec == PREC_F16W2 ? 2 : 1) +
+                       M * a.N * 4.0 * ((a.out ? 1 : 0) + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0)) +
+                       (act ? M * a.N * 2.0 : 0.0);
+  return tconv(a, (const u16*)a.w + 2 * a.w_lo_off, a.w_lo_off, a.kpad, act ? &E : nullptr, flops, bytes,
+               (hipStream_t)stream);
+}

@@ -346,17 +346,21 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
            act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False,
-           strided: Optional[tuple] = None):
+           strided: Optional[tuple] = None, dense: bool = False):
     """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
 
     act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
     planes (NP, B, T, round_up(N, 32)) from the fused epilogue -> (out or None, planes).
     strided = (out, stride, offset, pad): one ConvTranspose1d phase, row t -> row t*stride + offset of the
-    fp32 (B, R, N) tensor `out` (written in place and returned), input rows t - pad + tap*dilation."""
+    fp32 (B, R, N) tensor `out` (written in place and returned), input rows t - pad + tap*dilation.
+    dense = True: the narrow-stage resident-weight kernel (alcm_opconv_dense): weights packed with cpad = C_real
+    (pack_conv_weight(w)), planes channels >= C_real ignored, the fused Activation1d writes channels < N only."""
     npl, B, T, Cp = planes.shape
     assert planes.dtype == torch.int16 and planes.is_contiguous()
     N, cin, k = w.shape
     assert cin == C_real <= Cp
+    if dense and packed is None:
+        packed = pack_conv_weight(w)
     if packed is None:
         wp = torch.nn.functional.pad(w, (0, 0, 0, Cp - cin)).contiguous() if Cp != cin else w
         packed = pack_conv_weight(wp)
@@ -398,7 +402,10 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
         a.act_alpha_exp, a.act_inv_beta = ptr(ae), ptr(ib)
         a.act_up_filter = fu.data_ptr()
         a.act_down_filter = fd.data_ptr()
-    check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
+    if dense:
+        check(lib().alcm_opconv_dense(C.byref(a), stream_handle()), "opconv_dense")
+    else:
+        check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
     del keep
     if act is not None:
         return out, y

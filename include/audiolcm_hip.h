@@ -201,6 +201,13 @@ typedef struct alcm_opconv_args {
   int out_stride, out_offset, out_rows;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
+/* alcm_opconv_dense: the narrow AMPBlock conv of BigVGAN stages 3-5 (vocoder/bigvgan/models.py:72-81, C = N in
+ * {24, 48} at F16 / F16W2, 96 at F16; ksize <= 11, (ksize-1)*dil <= 64) with the weights resident in LDS: same
+ * arguments as alcm_opconv except that w is packed by alcm_pack_conv_weight with cpad = C (dense K = tap*C + c,
+ * kpad = round_up(ksize*C, 32)); the planes a may be wider (Cp > C: channels >= C are ignored) and the fused
+ * Activation1d writes only channels < N of its planes.  Epilogues: act (conv1), res + out + act (conv2), res + out
+ * with out_scale and accumulate, no act (a resblock's last conv2).  ALCM_E_INVALID for anything else. */
+int alcm_opconv_dense(const alcm_opconv_args* args, alcm_stream_t stream);
 
 /* alcm_flash_attention: multi-head self-attention of the DiT (CrossAttention with context = x,
  * ldm/modules/new_attention.py:89-130, the q/k/v projections already applied):

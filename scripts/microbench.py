@@ -282,6 +282,86 @@ def bench_tail(B=32):
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
 
 
+def bench_tailab(B=32):
+    """timing ablations of the tail convs as the model runs them (ALCM_OPCONV_ABLATE: 1 no epilogue, 2 no MFMA,
+    3 neither): conv1 + fused Activation1d, conv2 + residual + fused Activation1d, per tail stage, k = 11 / 3"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    for C, T, p in ((96, 39936, 2), (48, 79872, 3), (24, 159744, 3)):  # mixed-policy precisions
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        pl = K.operand_planes(x, p)
+        cp = (C + 31) // 32 * 32
+        for k, d in ((11, 5), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
+            line = []
+            for ab in os.environ.get("ABLATE", "0,1,2,3").split(","):
+                os.environ["ALCM_OPCONV_ABLATE"] = ab
+                _hip.reload_knobs()
+                ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
+                ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
+                line.append(f"ab{ab}: conv1+act {ms1:6.3f} conv2+res+act {ms2:6.3f}")
+            os.environ.pop("ALCM_OPCONV_ABLATE")
+            _hip.reload_knobs()
+            print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
+
+
+def bench_tconv(B=32):
+    """resident-weight narrow conv (alcm_opconv_dense) vs opconv_kernel / nconv on the tail shapes as the model runs
+    them (conv1 + fused Activation1d, conv2 + residual + fused Activation1d), with ALCM_TCONV_ABLATE variants
+    (1 no epilogue, 2 no MFMA, 4 no window DMA; timing only)"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    sel = os.environ.get("TC_SHAPES", "96,48,24")
+    for C, T, p in ((96, 39936, 2), (48, 79872, 3), (24, 159744, 3)):  # mixed-policy precisions
+        if str(C) not in sel.split(","):
+            continue
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        pl = K.operand_planes(x, p)
+        cp = (C + 31) // 32 * 32
+        for k, d in ((11, 5), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
+            pd = K.pack_conv_weight(w)
+            line = []
+            ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
+            ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
+            line.append(f"opconv: conv1+act {ms1:6.3f} conv2+res+act {ms2:6.3f}")
+            for ab in os.environ.get("ABLATE", "0,1,2,4").split(","):
+                os.environ["ALCM_TCONV_ABLATE"] = ab
+                _hip.reload_knobs()
+                ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pd, act=(a, bt, f, f), fp32_out=False,
+                                              dense=True))
+                ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pd, act=(a, bt, f, f),
+                                              dense=True))
+                line.append(f"dense ab{ab}: {ms1:6.3f} {ms2:6.3f}")
+            os.environ.pop("ALCM_TCONV_ABLATE")
+            _hip.reload_knobs()
+            print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
+
+
+def bench_tail1(B=32):
+    """3 launches of the stage-4 (C = 48, k = 11, d = 5, F16W2) conv2 + residual + fused Activation1d as the model
+    runs it, with the current ALCM_* settings (target of rocprofv3 --pmc passes)"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    C, T, p, k, d = int(os.environ.get("TC", "48")), int(os.environ.get("TT", "79872")), 3, 11, 5
+    x = torch.randn((B, T, C), device="cuda")
+    r = torch.randn((B, T, C), device="cuda")
+    a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+    pl = K.operand_planes(x, p)
+    cp = (C + 31) // 32 * 32
+    w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+    pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
+    for _ in range(3):
+        K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f))
+    torch.cuda.synchronize()
+
+
 def bench_attn(B=32):
     """DiT self-attention at the bench shape (L = 467, 8 heads x 72), fp16 operands"""
     L, H = 467, 576
@@ -331,4 +411,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

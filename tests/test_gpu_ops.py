@@ -430,3 +430,43 @@ def test_activation1d_op(K, C, T, prec):
     else:
         got = pl[0, ..., :C].view(torch.bfloat16).float() + pl[1, ..., :C].view(torch.bfloat16).float()
         assert rel_l2(got.numpy(), ref.numpy()) < 2e-5
+
+
+@pytest.mark.parametrize("C,T,k,dil,prec", [(24, 1000, 11, 5, 3), (48, 700, 7, 3, 3), (96, 500, 3, 1, 2),
+                                            (96, 333, 11, 5, 2), (24, 250, 3, 1, 2), (48, 2000, 11, 5, 2),
+                                            (48, 37, 3, 1, 3)])
+@pytest.mark.parametrize("mode", ["conv1", "conv2", "last"])
+def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
+    """alcm_opconv_dense (BigVGAN stages 3-5: dense K = tap*C + c, weights resident in LDS, persistent tiles) == the
+    Cp-padded opconv path on the same planes: conv1 (+ fused Activation1d), conv2 (+ residual, fp32 state, fused
+    Activation1d), a resblock's last conv2 (+ residual, out_scale, accumulate).  fp32 outputs differ by the K order
+    only (rel-L2 1e-5); the planes by fp16 rounding flips of those values (channels < N compared: the dense kernel
+    leaves the operand padding alone)."""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B = 2
+    x = _r((B, T, C), 60)
+    w, bias = _r((C, C, k), 61, 0.7 / np.sqrt(C * k)), _r((C,), 62, 0.05)
+    r = dev(_r((B, T, C), 63))
+    a, bt = dev(_r((C,), 64, 0.3)), dev(_r((C,), 65, 0.3))
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    pl = K.operand_planes(dev(x), prec)
+    dw = dev(w)
+
+    def dec(p):
+        return p[0, ..., :C].cpu().view(torch.float16).float().numpy()
+    if mode == "conv1":
+        _, pl_ref = K.opconv(pl, C, dw, dev(bias), dil, prec, act=(a, bt, f, f), fp32_out=False)
+        _, pl_d = K.opconv(pl, C, dw, dev(bias), dil, prec, act=(a, bt, f, f), fp32_out=False, dense=True)
+        assert np.isfinite(dec(pl_d)).all()
+        assert rel_l2(dec(pl_d), dec(pl_ref)) < 5e-4
+    elif mode == "conv2":
+        y_ref, pl_ref = K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, act=(a, bt, f, f))
+        y_d, pl_d = K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, act=(a, bt, f, f), dense=True)
+        assert rel_l2(y_d.cpu().numpy(), y_ref.cpu().numpy()) < 1e-5
+        assert rel_l2(dec(pl_d), dec(pl_ref)) < 5e-4
+    else:
+        o0 = _r((B, T, C), 66)
+        o_ref, o_d = dev(o0.clone()), dev(o0.clone())
+        K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_ref)
+        K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_d, dense=True)
+        assert rel_l2(o_d.cpu().numpy(), o_ref.cpu().numpy()) < 1e-5
