@@ -95,7 +95,10 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
-  int tconv = 1;                 // ALCM_TCONV: resident-weight narrow conv for BigVGAN stages 3-5 (0 = opconv / nconv)
+  int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
+  int tconv_wgs = 0;             // ALCM_TCONV_WGS: persistent workgroups per CU of tconv_kernel's grid (0 by shape)
+  int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
+                                 // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv
   int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
 };
 const Knobs& knobs();

@@ -42,6 +42,8 @@ static Knobs read_knobs() {
   k.tail_prefetch = env_int("ALCM_TAIL_PREFETCH", 1);
   k.opconv_ablate = env_int("ALCM_OPCONV_ABLATE", 0);
   k.tconv = env_int("ALCM_TCONV", 1);
+  k.tconv_wgs = env_int("ALCM_TCONV_WGS", 0);
+  k.tconv_bm = env_int("ALCM_TCONV_BM", 256);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   return k;
 }

@@ -56,6 +56,65 @@ __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
 }
 
+// conv tile epilogue shared by the resident- and streamed-weight kernels: v = acc + bias staged in LDS (`ot`, row
+// stride NS + 4 floats; the caller's barrier retired every K-loop read of that region), + residual (rv: the tile
+// rows' residual, prefetched as float4 element e = tid + i * NT), fp32 state / accumulated output of the owned rows,
+// Activation1d of the owned rows into the next conv's planes
+template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, bool RES, bool OUTW, bool ACC,
+          bool PRE = true>
+__device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const float (&bias_r)[TN],
+                                          const float4 (&rv)[PRE ? NRES : 1], float* ot, int wr0, int t0, int e0, int E,
+                                          int b, int n0, const TConvDev& P) {
+  constexpr int OTS = NS + 4;
+  const int tid = threadIdx.x, lane = tid & 63, q4 = lane >> 4, l16 = lane & 15;
+  // v = conv + bias -> LDS
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wr0 + i * 16 + q4 * 4 + r;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = j * 16 + l16;
+        if (n < NS) ot[m * OTS + n] = acc[i][j][r] + bias_r[j];
+      }
+    }
+  __syncthreads();
+  const int e_hi = min(e0 + E, P.T);
+  if constexpr (RES || OUTW || ACC) {
+    // + residual (all tile rows: the activation reads the halo rows too); fp32 state of the owned rows
+#pragma unroll
+    for (int i = 0; i < NRES; ++i) {
+      const int e = tid + i * NT;
+      if (e >= BM * (NS / 4)) break;
+      const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
+      const int t = t0 + m;
+      float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
+      if constexpr (RES) {
+        float4 r4;
+        if constexpr (PRE) r4 = rv[PRE ? i : 0];
+        else r4 = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + min(max(t, 0), P.T - 1)) * P.N + n0 + n);
+        v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
+        if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
+      }
+      if ((OUTW || ACC) && t >= e0 && t < e_hi) {
+        float* op = P.out + ((int64_t)b * P.T + t) * P.N + n0 + n;
+        if constexpr (ACC) {
+          v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
+          if (P.accumulate) {
+            const float4 pv = *reinterpret_cast<const float4*>(op);
+            v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
+          }
+        }
+        *reinterpret_cast<float4*>(op) = v;
+      }
+    }
+    if constexpr (ACT) __syncthreads();
+  }
+  if constexpr (ACT)
+    act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+}
+
 // C input channels, NS output channels per tile, NPB weight planes (1 = F16, 2 = F16W2), BM rows per tile,
 // R Activation1d rows per work item, WBYTES LDS bytes reserved for the weights (all planes)
 template <int C, int NS, int NPB, int BM, int R, int WBYTES, bool ACT, bool RES, bool OUTW, bool ACC>
@@ -72,6 +131,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
   constexpr int REGION = STAGE > WINB ? STAGE : WINB;   // window, then (after the K loop) the staged tile
   constexpr int SMEM = WBYTES + REGION;
   static_assert(SMEM <= 163840, "LDS");
+  static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
   static_assert(C % 8 == 0 && NS % 4 == 0, "geometry");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   char* const wl = smem;            // weights
@@ -196,51 +256,168 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
       continue;
     }
 
-    // ---- epilogue: v = conv + bias -> LDS
+    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P);
+    __syncthreads();  // staged-tile reads retired before the next window DMA overwrites the region
+  }
+}
+
+// Streamed-weight variant (ALCM_TCONV=2 / by shape): 4 waves of 64 rows x NS columns, the weights of each 32-deep K
+// slice DMA'd two slices ahead into a 4-slot LDS ring (one barrier per slice), <= 80 KB of LDS so two workgroups
+// share a CU: the Activation1d epilogue (VALU) of one overlaps the K loop (MFMA) of the other, which the
+// resident-weight kernel (one workgroup per CU at C >= 48) cannot do.  Ring slot layout: row n of 64 B (32 fp16 of
+// K), its 16-B piece q at physical piece q ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows).
+template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
+__global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TConvDev P) {
+  constexpr int NT = 256, RPW = BM / 4, TM = RPW / 16;
+  constexpr int NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
+  constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;
+  constexpr int RS = RSS * 16;
+  constexpr int WRMAX = BM + 64;
+  constexpr int WIN_INSTR = (WRMAX * RSS + 63) / 64;
+  constexpr int WPW = (WIN_INSTR + 3) / 4;              // window DMA instructions per wave (uniform)
+  constexpr int SLOT = NSP * 64 * NPB;                  // one K slice of every weight plane
+  constexpr int SPI = (NSP * 4 * NPB + 63) / 64;        // DMA instructions per slice
+  constexpr int DPW = (SPI + 3) / 4;                    // per wave (uniform: extra lanes write the scratch line)
+  constexpr int RING = 4;
+  constexpr int WINB = WPW * 4 * 1024;
+  constexpr int RINGB = RING * SLOT;
+  constexpr int OTS = NS + 4;
+  constexpr int STAGE = BM * OTS * 4;
+  constexpr int REGION = (STAGE > WINB + RINGB ? STAGE : WINB + RINGB);
+  constexpr int SMEM = REGION + 1024 * 4;               // + one scratch KB per wave for padding DMA instructions
+  static_assert(SMEM <= (BM <= 128 ? 54 * 1024 : 81920), "two (BM = 128: three) workgroups per CU");
+  static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
+  static_assert(C % 8 == 0 && NS % 4 == 0 && RPW % 16 == 0, "geometry");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  char* const win = smem;
+  char* const ring = smem + WINB;
+  char* const scratch = smem + REGION;
+  float* const ot = reinterpret_cast<float*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q4 = lane >> 4, l16 = lane & 15;
+  const int K = P.ksize, dil = P.dil;
+  const int nslice = P.kd / 32;
+  const int E = BM - 2 * ACT_EPI_HALO;
+  const int tile = blockIdx.x;
+  const int mt = tile / P.ncg, cg = tile - mt * P.ncg;
+  const int n0 = cg * NS;
+  const int b = mt / P.tiles_per_batch;
+  const int e0 = (mt - b * P.tiles_per_batch) * E;
+  const int t0 = e0 - ACT_EPI_HALO;
+  const int WR = BM + (K - 1) * dil;
+  const int wr0 = wave * RPW;
+
+  float bias_r[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
+  constexpr int NRES = (BM * (NS / 4) + NT - 1) / NT;
+  constexpr bool PRE = NRES <= 12;  // residual prefetched into registers (C = 96: loaded in the epilogue)
+  float4 rv[PRE ? NRES : 1];
+  if constexpr (RES && PRE) {
+#pragma unroll
+    for (int i = 0; i < NRES; ++i) {
+      const int e = tid + i * NT;
+      const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
+      const int t = min(max(t0 + m, 0), P.T - 1);
+      rv[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + t) * P.N + n0 + (e < BM * (NS / 4) ? n : 0));
+    }
+  }
+  // window: slot g -> row g / RSS, piece g % RSS
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int i = wave + 4 * j;
+    const int g = i * 64 + lane;
+    const int r = g / RSS, q = g - r * RSS;
+    const int ts = t0 - P.pad + r;
+    const bool ok = i < WIN_INSTR && r < WR && q < C / 8 && ts >= 0 && ts < P.T;
+    const u16* src = ok ? P.a + ((int64_t)b * P.T + ts) * P.Cp + q * 8 : reinterpret_cast<const u16*>(g_tconv_zero);
+    tc_glds16(src, win + i * 1024);
+  }
+  // weight slice s -> ring slot s % RING: instruction i covers slots 64 i .. 64 i + 63 of [plane][n][piece]
+  auto stage_slice = [&](int s) {
+    char* dst = ring + (s % RING) * SLOT;
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int i = wave + 4 * j;
+      const int g = i * 64 + lane;
+      const int p = g / (NSP * 4), gg = g - p * (NSP * 4);
+      const int n = gg >> 2, pq = gg & 3;
+      const int q = pq ^ ((n >> 2) & 3);
+      const bool ok = i < SPI && n < NS;
+      const u16* src = ok ? P.w + p * P.w_lo + (int64_t)(n0 + n) * P.kd + s * 32 + q * 8
+                          : reinterpret_cast<const u16*>(g_tconv_zero);
+      tc_glds16(src, i < SPI ? dst + i * 1024 : scratch + wave * 1024);
+    }
+  };
+  stage_slice(0);
+  if (nslice > 1) stage_slice(1);
+  if (nslice > 1) {
+    if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* arow = win + (wr0 + l16) * RS;
+  const int bsw = (l16 >> 2) & 3;
+  for (int s = 0; s < nslice; ++s) {
+    const bool more = s + 2 < nslice;
+    if (more) stage_slice(s + 2);
+    const int kk = s * 32 + q4 * 8;
+    int tap = kk / C;
+    const int c = kk - tap * C;
+    tap = min(tap, K - 1);
+    const char* bs = ring + (s % RING) * SLOT + l16 * 64 + ((q4 ^ bsw) << 4);
+    bf16x8 af[TM], bh[TN], bl[NPB == 2 ? TN : 1];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(bs + j * 16 * 64);
+      if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bs + NSP * 64 + j * 16 * 64);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dil) * RS + c * 2);
+    if (P.ablate & 2) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[j]));
+    } else {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (NPB == 2) acc[i][j] = mfma16<PREC_F16>(af[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_F16>(af[i], bh[j], acc[i][j]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // slice s + 1 (issued one slice earlier) has landed; slice s + 2 stays in flight across the barrier
+    if (more) {
+      if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  if (P.ablate & 1) {
+    float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wr0 + i * 16 + q4 * 4 + r;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = j * 16 + l16;
-          if (n < NS) ot[m * OTS + n] = acc[i][j][r] + bias_r[j];
-        }
-      }
-    __syncthreads();
-    const int e_hi = min(e0 + E, P.T);
-    if constexpr (RES || OUTW || ACC) {
-      // + residual (all tile rows: the activation reads the halo rows too); fp32 state of the owned rows
-#pragma unroll
-      for (int i = 0; i < NRES; ++i) {
-        const int e = tid + i * NT;
-        if (e >= BM * (NS / 4)) break;
-        const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
-        const int t = t0 + m;
-        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        if constexpr (RES) {
-          v.x += rv[i].x; v.y += rv[i].y; v.z += rv[i].z; v.w += rv[i].w;
-          if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
-        }
-        if ((OUTW || ACC) && t >= e0 && t < e_hi) {
-          float* op = P.out + ((int64_t)b * P.T + t) * P.N + n0 + n;
-          if constexpr (ACC) {
-            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
-            if (P.accumulate) {
-              const float4 pv = *reinterpret_cast<const float4*>(op);
-              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
-            }
-          }
-          *reinterpret_cast<float4*>(op) = v;
-        }
-      }
-      if constexpr (ACT) __syncthreads();
-    }
-    if constexpr (ACT)
-      act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
-    __syncthreads();  // staged-tile reads retired before the next window DMA overwrites the region
+      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 123.f && P.out) P.out[tid] = sum;
+    return;
   }
+  tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P);
 }
 
 // -------------------------------------------------------------------------------------------------- host
@@ -279,6 +456,16 @@ static int tc_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, b
   return 0;
 }
 
+template <int C, int NS, int NPB, int BM, int R>
+static int tc2_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
+  const dim3 g(grid), blk(256);
+  if (act && !res && !outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, false, false, false>), g, blk, 0, s, P);
+  else if (act && res && outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, true, true, false>), g, blk, 0, s, P);
+  else if (!act && res && acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, false, true, false, true>), g, blk, 0, s, P);
+  else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
+  return 0;
+}
+
 // conv on operand planes with dense fp16 weights `wd` ([N][kd], K = tap * C + c; lo plane wd_lo elements after
 // hi for F16W2): out / res fp32 [B][T][N], Activation1d of the result into act->plane (or none)
 int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const ActEpiDev* act, double flops,
@@ -303,34 +490,57 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   P.wslots = slots % 2 ? slots : slots + 1;
   const int npb = a.prec == PREC_F16W2 ? 2 : 1;
   const int C = a.C;
-  const int BM = C == 96 ? 192 : 256;
-  const int NS = C == 96 ? 48 : C;
+  // streamed weights (two workgroups per CU) where the resident weights would take a CU's LDS: C >= 48
+  const int tk = knobs().tconv;
+  // measured per launch (scripts/microbench.py tconv): streamed wins at C = 96 and C = 24, resident at C = 48
+  const bool streamed = tk == 2 || (tk != 3 && C != 48);
+  const bool small = streamed && C != 96 && knobs().tconv_bm == 128;  // 128-row tiles, three workgroups per CU
+  const int BM = small ? 128 : (C == 96 ? 192 : 256);
+  const int NS = (!streamed && C == 96) ? 48 : C;
   P.ncg = a.N / NS;
   P.tiles_per_batch = (a.T + (BM - 2 * ACT_EPI_HALO) - 1) / (BM - 2 * ACT_EPI_HALO);
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.ncg;
   if (nt >= (1ll << 30)) return set_error(ALCM_E_INVALID, "tconv: problem too large");
   P.ntiles = (int)nt;
-  // persistent: one workgroup per CU (the LDS holds the weights), a multiple of ncg so a workgroup's column group
-  // (blockIdx % ncg) is the same for every tile it takes (tile % ncg == blockIdx % ncg)
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  int grid = std::min<int64_t>(nt, (int64_t)ncu);
-  grid = std::max(P.ncg, grid / P.ncg * P.ncg);
   const bool outw = a.out && !acc_mode;
   void* tok = prof_start(s);
   int rc;
-  if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);
-  else if (C == 48) {
-    if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
-    else rc = tc_mode<48, 48, 1, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+  if (streamed) {
+    if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    else if (small && C == 48) {
+      if (npb == 2) rc = tc2_mode<48, 48, 2, 128, 14>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<48, 48, 1, 128, 14>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    } else if (small) {
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 128, 7>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 128, 7>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    } else if (C == 48) {
+      if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<48, 48, 1, 256, 24>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    } else {
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 12>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 256, 12>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    }
   } else {
-    if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
-    else rc = tc_mode<24, 24, 1, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+    // persistent: a multiple of ncg workgroups so a workgroup's column group (blockIdx % ncg) is the same for every
+    // tile it takes (tile % ncg == blockIdx % ncg); C = 24 fits two per CU
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int wgs = knobs().tconv_wgs > 0 ? knobs().tconv_wgs : (C == 24 ? 2 : 1);
+    int grid = std::min<int64_t>(nt, (int64_t)ncu * wgs);
+    grid = std::max(P.ncg, grid / P.ncg * P.ncg);
+    if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);
+    else if (C == 48) {
+      if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+      else rc = tc_mode<48, 48, 1, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+    } else {
+      if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+      else rc = tc_mode<24, 24, 1, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+    }
   }
   if (rc) return rc;
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::tconv_kernel<C%d, W%d, %s%s%s>", C, npb, act ? "act" : "",
+    std::snprintf(name, sizeof(name), "alcm::tconv%s_kernel<C%d, W%d, BM%d, %s%s%s>", streamed ? "2" : "", C, npb, BM, act ? "act" : "",
                   a.res ? "+res" : "", acc_mode ? "+acc" : "");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d k%d", a.T, a.ksize);

@@ -331,17 +331,41 @@ def bench_tconv(B=32):
             ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
             ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
             line.append(f"opconv: conv1+act {ms1:6.3f} conv2+res+act {ms2:6.3f}")
-            for ab in os.environ.get("ABLATE", "0,1,2,4").split(","):
-                os.environ["ALCM_TCONV_ABLATE"] = ab
+            for var in os.environ.get("VARS", "ALCM_TCONV=3,ALCM_TCONV=2").split(","):
+                kv = dict(x.split("=") for x in var.split("+"))
+                os.environ.update(kv)
                 _hip.reload_knobs()
                 ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pd, act=(a, bt, f, f), fp32_out=False,
                                               dense=True))
                 ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pd, act=(a, bt, f, f),
                                               dense=True))
-                line.append(f"dense ab{ab}: {ms1:6.3f} {ms2:6.3f}")
-            os.environ.pop("ALCM_TCONV_ABLATE")
+                line.append(f"{'/'.join(kv.values())}: {ms1:6.3f} {ms2:6.3f}")
+                for key in kv:
+                    os.environ.pop(key)
             _hip.reload_knobs()
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
+
+
+def bench_tail1d(B=32):
+    """3 launches of one dense narrow conv (alcm_opconv_dense) as the model runs it: TC channels, TK taps (dilation 5
+    for k = 11, else 1), TMODE conv1 (fused Activation1d) / conv2 (+ residual, fp32 state, fused Activation1d), with
+    the current ALCM_* settings (target of rocprofv3 --pmc passes)"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    C, k = int(os.environ.get("TC", "48")), int(os.environ.get("TK", "3"))
+    T = {96: 39936, 48: 79872, 24: 159744}[C]
+    d, p = (5 if k == 11 else 1), (2 if C == 96 else 3)
+    x = torch.randn((B, T, C), device="cuda")
+    r = torch.randn((B, T, C), device="cuda")
+    a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+    pl = K.operand_planes(x, p)
+    w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+    pd = K.pack_conv_weight(w)
+    conv2 = os.environ.get("TMODE", "conv1") == "conv2"
+    for _ in range(3):
+        K.opconv(pl, C, w, None, d, p, residual=r if conv2 else None, packed=pd, act=(a, bt, f, f),
+                 fp32_out=conv2, dense=True)
+    torch.cuda.synchronize()
 
 
 def bench_tail1(B=32):
@@ -411,4 +435,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
