@@ -67,6 +67,14 @@ struct ActEpiDev;
 int tconv(const alcm_opconv_args& a, const unsigned short* wd, int64_t wd_lo, int kd, const ActEpiDev* act,
           double flops, double bytes, hipStream_t s);
 
+// bf16x3 1x1 conv on split operand planes (alcm_sgemm.hip)
+bool sgemm_planes_ok(int K, int N, int kpad);
+int sgemm_planes(const unsigned short* a, int64_t a_lo, int M, int K, const unsigned short* w, int64_t w_lo, int kpad,
+                 int N, const float* bias, const float* res, int64_t ldr, float* out, int64_t ldo, float out_scale,
+                 hipStream_t s);
+int split_planes(const float* x, int64_t rows, int C, int T, const float* scale, const float* shift,
+                 unsigned short* y, hipStream_t s);
+
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
   int wconv = 8;                 // ALCM_WCONV: 8 = 2-workgroup/CU kernel, 5 = 256-row kernel, 0 = neither
@@ -95,6 +103,7 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
+  int sgemm = 1;                 // ALCM_SGEMM: DiT proj_in / proj_out on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
   int tconv_wgs = 0;             // ALCM_TCONV_WGS: persistent workgroups per CU of tconv_kernel's grid (0 by shape)
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,

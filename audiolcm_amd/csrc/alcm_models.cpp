@@ -819,7 +819,16 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
   for (const DitBlock& blk : D.blocks) {
     // TemporalTransformer (concatDiT.py:159-171): GN32 -> 1x1 -> block -> 1x1 -> +x
     ALCM_TRY(group_norm_affine(w.h, B, L, H, (int64_t)L * H, H, 32, 1e-6f, blk.gn.g, blk.gn.b, w.gsc, w.gsh, s));
-    {
+    // bf16x3 1x1 convs on split planes (alcm_sgemm.hip): the GroupNorm affine applied once while the planes are
+    // written; w.g is free outside the feed-forward
+    const bool sg = split == PREC_SPLIT && sgemm_planes_ok(H, H, blk.proj_in.w.kpad) &&
+                    sgemm_planes_ok(H, H, blk.proj_out.w.kpad) && blk.proj_in.w.cpad == H && blk.proj_out.w.cpad == H;
+    u16* spl = reinterpret_cast<u16*>(w.g);
+    if (sg) {
+      ALCM_TRY(split_planes(w.h, (int64_t)B * L, H, L, w.gsc, w.gsh, spl, s));
+      ALCM_TRY(sgemm_planes(spl, (int64_t)B * L * H, B * L, H, blk.proj_in.w.p, blk.proj_in.w.lo, blk.proj_in.w.kpad,
+                            H, blk.proj_in.b, nullptr, 0, w.u, H, 1.f, s));
+    } else {
       ConvOpts o;
       o.pro = Pro{w.gsc, w.gsh, H, nullptr, nullptr, 0};
       ALCM_TRY(conv(s, split, B, L, hv, blk.proj_in, uo, o));
@@ -893,7 +902,11 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       o2.res = ur;
       ALCM_TRY(conv(s, pff, B, L, cl(w.g, L, 4 * H), blk.ff2, uo, o2));
     }
-    {
+    if (sg) {
+      ALCM_TRY(split_planes(w.u, (int64_t)B * L, H, 0, nullptr, nullptr, spl, s));
+      ALCM_TRY(sgemm_planes(spl, (int64_t)B * L * H, B * L, H, blk.proj_out.w.p, blk.proj_out.w.lo,
+                            blk.proj_out.w.kpad, H, blk.proj_out.b, w.h, H, w.h, H, 1.f, s));
+    } else {
       ConvOpts o;
       o.res = hr;
       ALCM_TRY(conv(s, split, B, L, uv, blk.proj_out, ho, o));
@@ -960,6 +973,23 @@ static VaeWs plan_vae(const VaeW& V, Bump& bp, int B, int T) {
   return w;
 }
 
+// bf16x3 1x1 conv through split operand planes (alcm_sgemm.hip) when the layer qualifies: out[b,t,:] =
+// W (x[b,t,:] (* scale[b] + shift[b])) + bias (+ res), rows of ld C in / ldo out; `scratch` holds B*T*C*4 bytes of
+// planes.  Returns 1 when it ran, 0 when the caller should use conv(), or an error code (negative never)
+static int split_1x1(hipStream_t s, int prec, int B, int T, const float* x, int C, const float* scale,
+                     const float* shift, const ConvW& cw, const float* res, float* out, int ldo, u16* scratch,
+                     int* rc) {
+  *rc = 0;
+  if (prec != PREC_SPLIT || !scratch || cw.w.taps != 1 || cw.w.cpad != C || cw.w.cin != C ||
+      !sgemm_planes_ok(C, cw.w.rows, cw.w.kpad))
+    return 0;
+  const int64_t rows = (int64_t)B * T;
+  if ((*rc = split_planes(x, rows, C, T, scale, shift, scratch, s))) return 1;
+  *rc = sgemm_planes(scratch, rows * C, (int)rows, C, cw.w.p, cw.w.lo, cw.w.kpad, cw.w.rows, cw.b, res, ldo, out,
+                     ldo, 1.f, s);
+  return 1;
+}
+
 // ResnetBlock1D (autoencoder1d.py:212-235): out = x' + conv2(swish(GN(conv1(swish(GN(x))))))
 static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& r, const float* x, float* tmp,
                    float* sc, float* out, VaeWs& w) {
@@ -972,7 +1002,11 @@ static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& 
                                w.gsh, s));
     const float* resid = x;
     if (r.has_nin) {
-      ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.nin, ocl(sc, T, r.cout), ConvOpts{}));
+      int rc;  // `out` is free until conv2 writes it: the split planes of x go there
+      if (!split_1x1(s, split, B, T, x, r.cin, nullptr, nullptr, r.nin, nullptr, sc, r.cout,
+                     reinterpret_cast<u16*>(out), &rc))
+        ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.nin, ocl(sc, T, r.cout), ConvOpts{}));
+      ALCM_TRY(rc);
       resid = sc;
     }
     ALCM_TRY(affine_plane(tmp, B, T, r.cout, 1, w.gsc, w.gsh, 1, w.pl, pk3, s));
@@ -985,7 +1019,11 @@ static int vae_res(hipStream_t s, int split, int pk3, int B, int T, const ResW& 
   ALCM_TRY(group_norm_affine(tmp, B, T, r.cout, (int64_t)T * r.cout, r.cout, 32, 1e-6f, r.n2.g, r.n2.b, w.gsc, w.gsh, s));
   const float* resid = x;
   if (r.has_nin) {
-    ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.nin, ocl(sc, T, r.cout), ConvOpts{}));
+    int rc;
+    if (!split_1x1(s, split, B, T, x, r.cin, nullptr, nullptr, r.nin, nullptr, sc, r.cout, reinterpret_cast<u16*>(out),
+                   &rc))
+      ALCM_TRY(conv(s, split, B, T, cl(x, T, r.cin), r.nin, ocl(sc, T, r.cout), ConvOpts{}));
+    ALCM_TRY(rc);
     resid = sc;
   }
   ConvOpts o2;
@@ -1067,9 +1105,13 @@ static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& 
   if (o_scratch == h) return set_error(ALCM_E_INVALID, "vae_attn: scratch aliases the activation");
   {
     ALCM_TRY(group_norm_affine(h, B, T, C, (int64_t)T * C, C, 32, 1e-6f, nw.g, nw.b, w.gsc, w.gsh, s));
-    ConvOpts o;
-    o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, 0};
-    ALCM_TRY(conv(s, split, B, T, cl(h, T, C), qkvw, ocl(w.qkv, T, 3 * C), o));
+    int rc;  // w.b (the ResnetBlock1D scratch) is free here: the split planes go there
+    if (!split_1x1(s, split, B, T, h, C, w.gsc, w.gsh, qkvw, nullptr, w.qkv, 3 * C, reinterpret_cast<u16*>(w.b), &rc)) {
+      ConvOpts o;
+      o.pro = Pro{w.gsc, w.gsh, C, nullptr, nullptr, 0};
+      ALCM_TRY(conv(s, split, B, T, cl(h, T, C), qkvw, ocl(w.qkv, T, 3 * C), o));
+    }
+    ALCM_TRY(rc);
     const int Tp = round_up(T, 8);
     alcm_gemm_args g;
     std::memset(&g, 0, sizeof(g));
@@ -1095,9 +1137,12 @@ static int vae_attn(hipStream_t s, int split, int B, int T, int C, const NormW& 
     p.out = o_scratch; p.o_st = C; p.o_sc = 1; p.o_zs1 = (int64_t)T * C; p.out_rows_per_batch = T; p.out_step = 1;
     p.prec = split;
     ALCM_TRY(gemm(p, s));
-    ConvOpts oo;
-    oo.res = Res{h, (int64_t)T * C, C, 1};
-    ALCM_TRY(conv(s, split, B, T, cl(o_scratch, T, C), ow, ocl(h, T, C), oo));
+    if (!split_1x1(s, split, B, T, o_scratch, C, nullptr, nullptr, ow, h, h, C, reinterpret_cast<u16*>(w.b), &rc)) {
+      ConvOpts oo;
+      oo.res = Res{h, (int64_t)T * C, C, 1};
+      ALCM_TRY(conv(s, split, B, T, cl(o_scratch, T, C), ow, ocl(h, T, C), oo));
+    }
+    ALCM_TRY(rc);
   }
   return 0;
 }
