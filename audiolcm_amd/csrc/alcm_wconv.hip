@@ -716,6 +716,345 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Persistent 8-wave wide conv (ALCM_WCONV3): one 512-thread workgroup per CU walks its tiles of 256 rows x 192
+// columns as ONE flat sequence of (tile, 64-channel chunk, tap) steps, so the staging pipeline never drains at a
+// tile boundary.  Waves 4 (M) x 2 (N), each 64 x 96 of 16x16x32 MFMAs (24 per 32-deep slice, two slices a step).
+//   * LDS (152 KB): input windows (256 + (k-1)d <= 320 rows x 128 B) double-buffered, weight tiles (192 x 128 B) in
+//     a 3-slot ring.  Images lane-linear with the 16-B slot swizzle s ^ (r & 7) (conflict-free ds_read_b128).
+//   * ONE barrier per step, in its middle (after the first slice's MFMAs are issued), behind a COUNTED vmcnt wait
+//     for the next step's weight tile (and, at a chunk's last step, the next chunk's window): every fragment the
+//     second slice and the next step's first slice read is then resident, so all fragment reads are issued a whole
+//     slice (24 MFMAs) ahead of their use — B fragments double-buffered in registers, A fragments replaced row by
+//     row as their last MFMA issues.  Right after that barrier the slot and window this step has finished reading
+//     are refilled: weight step g + 3 (2.5 steps of DMA latency hidden), and at a chunk's last step the window two
+//     chunks ahead (for a tile's last chunks: the next tile's).
+//   * the epilogue of a tile runs straight from the accumulators (no LDS, no barrier) while the next tile's first
+//     window and weight steps are already in flight;
+//   * per-CU L2 -> LDS bytes per MFMA flop: weights 1/256, window 1/(192 k): at k = 11 / 3, 18 / 24 B per cycle at
+//     the full MFMA rate, under the ~29 B/cycle a CU gathers from its L2 (MI355X_MICROARCH.md, "Indexed rows"),
+//     where the two-workgroup 256 x 96 / 128 x 192 tiles need 20-41.
+// Persistent order: XCD x owns the tile range [x R, (x+1) R) (R = ceil(tiles / 8)), its workgroups take every
+// (grid / 8)-th tile of it, N-major (concurrent tiles share a weight slice in the XCD's L2) or M-major.
+constexpr int W3_BM = 256, W3_BN = 192, W3_WROWS = 320;
+constexpr int W3_WBUF = W3_WROWS * 128;  // 40 KB
+constexpr int W3_BBUF = W3_BN * 128;     // 24 KB
+constexpr int W3_WPW = W3_WROWS / 8 / 8;  // window DMA instructions per wave (5)
+constexpr int W3_BPW = W3_BN / 8 / 8;     // weight DMA instructions per wave per step (3)
+
+template <int N>
+__device__ __forceinline__ void w3_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+// counted wait for n in {0, 3, 5, 6, 8, 11} (the only counts the schedule produces), then the barrier
+__device__ __forceinline__ void w3_wait_barrier_n(int n) {
+  switch (n) {
+    case 3: w3_wait_barrier<3>(); break;
+    case 5: w3_wait_barrier<5>(); break;
+    case 6: w3_wait_barrier<6>(); break;
+    case 8: w3_wait_barrier<8>(); break;
+    case 11: w3_wait_barrier<11>(); break;
+    default: w3_wait_barrier<0>(); break;
+  }
+}
+
+// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA
+template <int PREC, int AB>
+__global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
+  constexpr int TM = 4, TN = 6;
+  constexpr bool ab_dma = (AB & 4) != 0;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  const int ntiles = P.nwg;
+  const int R = (ntiles + 7) >> 3;
+  const int tbeg = xcd * R, tend = min(tbeg + R, ntiles);
+  const int first = tbeg + slot;
+  const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
+  if (my_n == 0) return;
+  const int K = P.ksize, Cp = P.Cp, nC = Cp / 64;
+  const int WR = W3_BM + (K - 1) * P.dil;
+  const int total = my_n * nC * K;   // steps
+  const int nchunks = my_n * nC;     // windows
+  const int tiles_m = ntiles / P.tiles_n;
+  auto tile_of = [&](int ti, int& b, int& t0, int& col0) {
+    const int tile = first + ti * nslot;
+    int mt, nt;
+    if (P.n_major) {
+      nt = tile / tiles_m;
+      mt = tile - nt * tiles_m;
+    } else {
+      mt = tile / P.tiles_n;
+      nt = tile - mt * P.tiles_n;
+    }
+    b = mt / P.tiles_per_batch;
+    t0 = (mt - b * P.tiles_per_batch) * W3_BM;
+    col0 = nt * W3_BN;
+  };
+  // window of global chunk q (tile q / nC, channel chunk q % nC) -> buffer q & 1
+  auto stage_win = [&](int q) {
+    const int ti = q / nC, c = q - ti * nC;
+    int b, t0, col0;
+    tile_of(ti, b, t0, col0);
+#pragma unroll
+    for (int j = 0; j < W3_WPW; ++j) {
+      const int row = 8 * (wave + 8 * j) + (lane >> 3);
+      const int ls = (lane & 7) ^ (row & 7);
+      const int ts = t0 - P.pad + row;
+      const bool ok = row < WR && ts >= 0 && ts < P.T;
+      const u16* src = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + c * 64 + ls * 8
+                          : reinterpret_cast<const u16*>(g_wconv_zero);
+      glds16(src, smem + (q & 1) * W3_WBUF + (wave + 8 * j) * 1024);
+    }
+  };
+  // weight-row DMA geometry (fixed per lane): instruction j covers rows 8 (wave + 8 j) .. + 7
+  int64_t boff[W3_BPW];
+#pragma unroll
+  for (int j = 0; j < W3_BPW; ++j) {
+    const int n = 8 * (wave + 8 * j) + (lane >> 3);
+    boff[j] = (int64_t)n * P.kpad + ((lane & 7) ^ (n & 7)) * 8;
+  }
+  // issue cursor: weight step ig = (tile iti, chunk ic, tap itap) -> slot ig % 3
+  int ig = 0, ic = 0, itap = 0, iti = 0, icol0;
+  {
+    int b_, t0_;
+    tile_of(0, b_, t0_, icol0);
+  }
+  auto issue_wt = [&](int sl) {
+    const u16* base = P.w + (int64_t)icol0 * P.kpad + itap * Cp + ic * 64;
+#pragma unroll
+    for (int j = 0; j < W3_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 8 * j) * 1024);
+    ++ig;
+    if (++itap == K) {
+      itap = 0;
+      if (++ic == nC) {
+        ic = 0;
+        if (++iti < my_n) {
+          int b_, t0_;
+          tile_of(iti, b_, t0_, icol0);
+        }
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int arow0 = wm * 64 + (lane & 15);
+  const int nrow0 = wn * 96 + (lane & 15);
+  const int bsw = lane & 7;
+  auto rdA = [&](int buf, int tp, int sub, int i) -> bf16x8 {
+    const int arow = arow0 + tp * P.dil;
+    return *reinterpret_cast<const bf16x8*>(smem + buf * W3_WBUF + arow * 128 +
+                                            (((4 * sub + (lane >> 4)) ^ (arow & 7)) << 4) + i * 16 * 128);
+  };
+  auto rdB = [&](int sl, int sub, int j) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(smem + 2 * W3_WBUF + sl * W3_BBUF + nrow0 * 128 +
+                                            (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
+  };
+
+  // prologue: window 0, weight 0, window 1, weight 1, weight 2 (in this order: the mid-step waits count on it)
+  stage_win(0);
+  issue_wt(0);
+  int pend = 0;  // vm instructions issued after the ones the next wait needs
+  if (nchunks > 1) {
+    stage_win(1);
+    pend += W3_WPW;
+  }
+  if (total > 1) {
+    issue_wt(1);
+    pend += W3_BPW;
+  }
+  if (total > 2) {
+    issue_wt(2);
+    pend += W3_BPW;
+  }
+  w3_wait_barrier_n(pend);
+  pend = total > 2 ? W3_BPW : 0;  // at step 0's mid wait (for weight 1): weight 2 may stay in flight
+
+  bf16x8 af[TM], bA[TN], bB[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) af[i] = rdA(0, 0, 0, i);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
+
+  int ti = 0, c = 0, tap = 0, sl = 0, q = 0;  // q: global chunk (window buffer q & 1)
+  for (int g = 0; g < total; ++g) {
+    // ---- slice 0: MFMAs on (af, bA); slice 1's B fragments (this slot) and A fragments (row by row) read under them
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bA[j], acc[i][j]);
+      af[i] = rdA(q & 1, tap, 1, i);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+
+    // ---- mid-step: weight step g + 1 (and at a chunk's last step the next chunk's window) resident in every
+    //      wave's share; every wave done reading this slot and, at a chunk's last step, this chunk's window
+    const bool chunk_end = tap == K - 1;
+    if (g + 1 < total) w3_wait_barrier_n(pend);
+    pend = 0;
+    if constexpr (!ab_dma) {
+      if (chunk_end && q + 2 < nchunks) {
+        stage_win(q + 2);
+        pend += W3_WPW;
+      }
+      if (ig < total) {
+        issue_wt(sl);
+        pend += W3_BPW;
+      }
+    }
+
+    // ---- slice 1: MFMAs on (af, bB); the next step's slice-0 fragments read under them
+    const int sl1 = sl == 2 ? 0 : sl + 1;
+    const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
+    const int ntap = chunk_end ? 0 : tap + 1;
+    // (after the last step these re-read resident LDS: harmless)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bB[j], acc[i][j]);
+      af[i] = rdA(nbuf, ntap, 0, i);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+
+    sl = sl1;
+    if (!chunk_end) {
+      ++tap;
+      continue;
+    }
+    tap = 0;
+    ++q;
+    if (++c == nC) {
+      // ---- tile epilogue, straight from the accumulators (fp32 out = (acc + bias + res) * scale (+ out))
+      if constexpr ((AB & 1) == 0) {
+        int b, t0, col0;
+        tile_of(ti, b, t0, col0);
+        float bv[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float rv[4][TN], pv[4][TN];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = min(t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r, P.T - 1);
+            const int64_t ro = ((int64_t)b * P.T + t) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
+              pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            if (t >= P.T) continue;
+            const int64_t ro = ((int64_t)b * P.T + t) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
+          }
+        }
+      } else {
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (sum == 123.f) P.out[tid] = sum;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c = 0;
+      ++ti;
+    }
+  }
+}
+
+static int g_ncu = 0;
+
+// Eligible: fp16 / bf16 operands, Cp % 64 == 0, 2 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
+// residual, scale, accumulate; no GEGLU / strided / fused activation).  Returns 1 when it launched.
+static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
+  if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
+  if (a.out_act || a.geglu_plane || a.out_stride > 0 || a.Cp % 64 || a.ksize < 2 || (a.ksize - 1) * a.dil > 64 ||
+      a.N % W3_BN || !a.out)
+    return 0;
+  if (!g_ncu) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                hipSuccess && n >= 8)
+      g_ncu = n;
+    else
+      g_ncu = 256;
+  }
+  WConvDev P{};
+  P.a = (const u16*)a.a;
+  P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
+  P.w = wplane; P.kpad = a.kpad; P.N = a.N;
+  P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+  P.tiles_per_batch = (a.T + W3_BM - 1) / W3_BM;
+  P.tiles_n = a.N / W3_BN;
+  const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
+  if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
+  P.nwg = (int)nt;
+  const int ord = knobs().wconv_order;
+  P.n_major = ord >= 0 ? ord : 1;
+  const int R = (P.nwg + 7) / 8;
+  int grid = 8 * std::min(g_ncu / 8, R);
+  if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
+  void* tok = prof_start(s);
+  const int ab = knobs().wconv_ablate;
+  if (ab && a.prec == PREC_F16) {
+    switch (ab) {
+#define W3AB(v) case v: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, v>), dim3(grid), dim3(512), 0, s, P); break;
+      W3AB(1) W3AB(4) W3AB(5)
+#undef W3AB
+      default: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P); break;
+    }
+  } else {
+    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0>), dim3(grid), dim3(512), 0, s, P);
+  }
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0>", a.prec);
+    if (knobs().prof_shapes)
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
+                    a.ksize);
+    prof_stop(tok, s, name, flops, bytes);
+  }
+  return 1;
+}
+
 // wconv2 tile by shape (ALCM_WCONV_TILE = -1): 256 x 96 where the weight stream dominates the per-CU fetch (k >= 7:
 // the window is amortised over >= 7 taps) and there is at least one 256-row tile per CU; 128 x 192 elsewhere.
 // Measured per launch (B = 32, scripts/microbench.py wablate, one box): s0 C768 k11 0.946 -> 0.860 ms, s1 C384 k11
@@ -730,6 +1069,8 @@ static bool wconv2_tile256(const alcm_opconv_args& a) {
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
   const int var = knobs().wconv;
+  if (knobs().wconv3 && !actepi && !a.geglu_plane && a.out_stride <= 0 && wconv3_try(a, wplane, flops, bytes, s))
+    return 1;
   const bool strided = a.out_stride > 0;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;
   if (var <= 0 && !act && !a.geglu_plane && !strided) return 0;

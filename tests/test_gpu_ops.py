@@ -334,6 +334,39 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
         assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("C,T,k,dil,grid", [(384, 1100, 7, 3, 0), (384, 1100, 7, 3, 8), (192, 1500, 3, 1, 16),
+                                            (768, 600, 11, 5, 8), (576, 467, 9, 1, 0)])
+@pytest.mark.parametrize("prec", [0, 2])
+def test_wconv3_persistent(K, C, T, k, dil, grid, prec, monkeypatch):
+    """Persistent 8-wave wide conv (ALCM_WCONV3: one flat (tile, chunk, tap) pipeline per workgroup, epilogue from
+    the accumulators) vs F.conv1d and vs the two-workgroup kernel on the same planes (same per-element product order:
+    bit-identical); ALCM_WCONV3_GRID caps the workgroups so each walks several tiles (cross-tile prefetch)."""
+    from audiolcm_amd import _hip
+    B = 2
+    x = _r((B, T, C), 90)
+    w, bias = _r((C, C, k), 91, 0.7 / np.sqrt(C * k)), _r((C,), 92, 0.05)
+    r = _r((B, T, C), 93)
+    ref = (F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1) + r) * 0.5
+    pl = K.operand_planes(dev(x), prec)
+
+    def run():
+        acc = dev(torch.ones((B, T, C)))
+        return K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
+                        accumulate_into=acc).cpu() - 1
+    y2 = run()
+    monkeypatch.setenv("ALCM_WCONV3", "1")
+    monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
+    _hip.reload_knobs()
+    try:
+        y3 = run()
+    finally:
+        monkeypatch.delenv("ALCM_WCONV3")
+        monkeypatch.delenv("ALCM_WCONV3_GRID")
+        _hip.reload_knobs()
+    assert rel_l2(y3.numpy(), ref.numpy()) < TOL[prec]
+    assert rel_l2(y3.numpy(), y2.numpy()) < 1e-6
+
+
 @pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
                                                  (192, 96, 900, 2, 2), (96, 48, 333, 2, 0)])
 def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
