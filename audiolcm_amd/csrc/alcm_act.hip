@@ -26,6 +26,12 @@ namespace alcm {
 // output rows and 256-B input row segments) where Cp allows, else NP = 16.
 constexpr int AC_SEG = 18;                 // upsampled samples per phase-1 thread (even: static FIR indexing)
 
+// 8-byte load at a 32-bit byte offset from a workgroup-uniform base: the saddr + voffset address form, no 64-bit
+// per-lane address arithmetic
+__device__ __forceinline__ f32x2 ld_f32x2(const float* base, uint32_t byte_off) {
+  return *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 template <int PREC, int AC_NP>
 __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__ x, u16* __restrict__ y,
                                                        int64_t y_lo, int T, int C, int Cp,
@@ -49,7 +55,10 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   const int p = tid % AC_NP;
   const int c = c0 + 2 * p;
   const bool live = c < C;  // pairs at or beyond C: operand padding (zeros)
-  const float* xb = x + ((int64_t)b * T) * C + (live ? c : 0);
+  // per-batch bases are workgroup-uniform (SGPRs); per-lane offsets stay 32-bit (a batch is < 2^31 elements), so
+  // each load / store is a saddr + 32-bit voffset access instead of a 64-bit multiply-add per address
+  const float* xb = x + ((int64_t)b * T) * C;
+  const int xc = live ? c : 0;
   const f32x2 ear = live ? f32x2{aexp[c], aexp[c + 1]} * INV_PI : f32x2{0.f, 0.f};
   const f32x2 h = live ? f32x2{ibeta[c], ibeta[c + 1]} * 0.5f : f32x2{0.f, 0.f};
   const int m0 = 2 * t0 - 6;  // sample index 0 of the tile (even); output j reads m = 2j - 5 .. 2j + 6
@@ -62,8 +71,9 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
     const int xlo = mb / 2 - 3;  // sample mb + q reads x rows xlo + (q + 5 - ku) / 2 + 3 - 3
     if (mb >= 0 && mb + AC_SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1) {
       f32x2 win[15];
+      const uint32_t o0 = (uint32_t)(xlo * C + xc);
 #pragma unroll
-      for (int i = 0; i < 15; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(xlo + i) * C);
+      for (int i = 0; i < 15; ++i) win[i] = ld_f32x2(xb, (o0 + (uint32_t)(i * C)) * 4u);
       // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
       // order compiles to 6-deep dependent chains with a wait state between links)
       f32x2 u[AC_SEG];
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
           const int ku = 2 * kk + ((m & 1) ? 0 : 1);
           int xi = (m + 5 - ku) / 2;
           xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
-          u = fma2(f32x2{f.up[ku], f.up[ku]}, *reinterpret_cast<const f32x2*>(xb + (int64_t)xi * C), u);
+          u = fma2(f32x2{f.up[ku], f.up[ku]}, ld_f32x2(xb, (uint32_t)(xi * C + xc) * 4u), u);
         }
         sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
       }
@@ -98,10 +108,10 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   const int run = tid / AC_NP;
   const int j0 = t0 + run * 8;
   if (j0 >= T) return;
-  u16* yb = y + ((int64_t)b * T) * Cp + c;
+  u16* yb = y + ((int64_t)b * T) * Cp;
   const int jn = min(8, T - j0);
   if (!live) {
-    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, f32x2{0.f, 0.f});
+    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (uint32_t)((j0 + r) * Cp + c), y_lo, f32x2{0.f, 0.f});
     return;
   }
   const f32x2* sp = sv + (2 * (j0 - t0) + 1) * AC_RS + p;
@@ -117,11 +127,13 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   for (int k = 0; k < 12; ++k)
 #pragma unroll
     for (int r = 0; r < 8; ++r) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, s[2 * r + k], o[r]);
+  const uint32_t yo = (uint32_t)(j0 * Cp + c) * 2u;  // byte offset from the uniform batch base
+  auto yp = [&](int r) { return reinterpret_cast<u16*>(reinterpret_cast<char*>(yb) + (yo + (uint32_t)(r * Cp) * 2u)); };
   if (jn == 8) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
+    for (int r = 0; r < 8; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
   } else {
-    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
+    for (int r = 0; r < jn; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
   }
 }
 

@@ -17,14 +17,16 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// x + h - h*cos(2*pi*fract(x*ea_rev)): SnakeBeta (activations.py:62-119) with h = inv_beta/2,
-// ea_rev = exp(alpha)/pi, since sin^2(z) = 1/2 - cos(2z)/2 and v_cos_f32 takes revolutions
-// (fract: one v_fract_f32 instead of rint + sub; the argument error it adds is < 6e-8 revolutions)
+// x + h - h*cos(2*pi*x*ea_rev): SnakeBeta (activations.py:62-119) with h = inv_beta/2, ea_rev = exp(alpha)/pi,
+// since sin^2(z) = 1/2 - cos(2z)/2 and v_cos_f32 takes revolutions.  No explicit argument reduction: v_cos_f32
+// reduces the argument itself — measured on gfx950 (scripts/probes/cos_probe.hip) its result equals
+// cos(2 pi fract(z)) within 6e-8 and a float64 cos within 1.2e-7 for |z| up to 4096 revolutions, so the
+// v_fract_f32 the previous form spent per sample (10 % of Activation1d's VALU cycles) bought nothing
 __device__ __forceinline__ f32x2 snake2(f32x2 u, f32x2 ear, f32x2 h) {
   const f32x2 z = u * ear;
   f32x2 c;
-  c.x = __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(z.x));
-  c.y = __builtin_amdgcn_cosf(__builtin_amdgcn_fractf(z.y));
+  c.x = __builtin_amdgcn_cosf(z.x);
+  c.y = __builtin_amdgcn_cosf(z.y);
   return fma2(-h, c, u + h);
 }
 
@@ -177,12 +179,15 @@ __device__ __forceinline__ void act_epilogue_ct(const float* tile, int ots, int 
                                                 int c0, int b, const ActEpiDev& A, int tid, int nthr) {
   constexpr float INV_PI = 0.318309886183790671538f;
   const int nrun = (e_hi - e_lo + R - 1) / R;
+  // the batch's plane base is uniform; per-item byte offsets stay 32-bit (a batch's plane is < 4 GB), so the stores
+  // need no 64-bit per-lane address arithmetic
+  char* const pb = reinterpret_cast<char*>(A.plane + ((int64_t)b * T) * A.Cp);
   for (int w = tid; w < NP * nrun; w += nthr) {
     const int run = w / NP, p = w - run * NP;
     const int c = c0 + 2 * p;
     const int j0 = e_lo + run * R;
     const int jn = min(R, e_hi - j0);
-    u16* yb = A.plane + ((int64_t)b * T) * A.Cp + c;
+    const uint32_t yo = (uint32_t)(j0 * A.Cp + c) * 2u, ys = (uint32_t)A.Cp * 2u;
     const float* col = tile + 2 * p;
     const f32x2 ear = f32x2{A.aexp[c], A.aexp[c + 1]} * INV_PI;
     const f32x2 h = f32x2{A.ibeta[c], A.ibeta[c + 1]} * 0.5f;
@@ -193,13 +198,13 @@ __device__ __forceinline__ void act_epilogue_ct(const float* tile, int ots, int 
       f32x2 o[R];
       act_run_interior<R>(win, A.f, ear, h, o);
 #pragma unroll
-      for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o[r]);
+      for (int r = 0; r < R; ++r) op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o[r]);
     } else {
       for (int r = 0; r < jn; ++r) {
         const f32x2 o = act_one_clamped(j0 + r, T, A.f, ear, h, [&](int i) {
           return *reinterpret_cast<const f32x2*>(col + (i - trow0) * ots);
         });
-        op_store2<PREC>(yb + (int64_t)(j0 + r) * A.Cp, A.plane_lo, o);
+        op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o);
       }
     }
   }

@@ -81,7 +81,7 @@ struct Knobs {
   int wconv_order = -1;          // ALCM_WCONV_ORDER: wconv2 workgroup order (-1 by shape, 0 M-tile major, 1 N-tile major)
   int wconv_ablate = 0;          // ALCM_WCONV_ABLATE: timing-only ablation bits of the wide-layer kernel
   int wconv_fpipe = 1;           // ALCM_WCONV_FPIPE: wconv2 fragment-pipelined K loop (0 = per-slice read-then-MFMA)
-  int wconv3 = 0;                // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip) where eligible
+  int wconv3 = -1;               // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip): -1 by shape, 0 off, 1 on
   int wconv3_grid = 0;           // ALCM_WCONV3_GRID: cap on wconv3's persistent workgroups (tests; 0 = one per CU)
   int wconv_tile = -1;           // ALCM_WCONV_TILE: wconv2 tile, 0 = 128 x 192, 1 = 256 x 96, -1 = by shape
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width

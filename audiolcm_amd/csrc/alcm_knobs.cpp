@@ -22,7 +22,7 @@ static Knobs read_knobs() {
   k.wconv_order = env_int("ALCM_WCONV_ORDER", -1);
   k.wconv_tile = env_int("ALCM_WCONV_TILE", -1);
   k.wconv_fpipe = env_int("ALCM_WCONV_FPIPE", 1);
-  k.wconv3 = env_int("ALCM_WCONV3", 0);
+  k.wconv3 = env_int("ALCM_WCONV3", -1);
   k.wconv3_grid = env_int("ALCM_WCONV3_GRID", 0);
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);

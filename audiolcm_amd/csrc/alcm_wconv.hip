@@ -742,22 +742,14 @@ constexpr int W3_BBUF = W3_BN * 128;     // 24 KB
 constexpr int W3_WPW = W3_WROWS / 8 / 8;  // window DMA instructions per wave (5)
 constexpr int W3_BPW = W3_BN / 8 / 8;     // weight DMA instructions per wave per step (3)
 
+// s_waitcnt vmcnt(N) lgkmcnt(0) through the builtin (the compiler's wait insertion sees it and does not re-wait for
+// LDS reads it already retired), then the barrier
 template <int N>
 __device__ __forceinline__ void w3_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  static_assert(N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
+  __builtin_amdgcn_s_barrier();
 }
-// counted wait for n in {0, 3, 5, 6, 8, 11} (the only counts the schedule produces), then the barrier
-__device__ __forceinline__ void w3_wait_barrier_n(int n) {
-  switch (n) {
-    case 3: w3_wait_barrier<3>(); break;
-    case 5: w3_wait_barrier<5>(); break;
-    case 6: w3_wait_barrier<6>(); break;
-    case 8: w3_wait_barrier<8>(); break;
-    case 11: w3_wait_barrier<11>(); break;
-    default: w3_wait_barrier<0>(); break;
-  }
-}
-
 // AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA
 template <int PREC, int AB>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
@@ -809,32 +801,40 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
       glds16(src, smem + (q & 1) * W3_WBUF + (wave + 8 * j) * 1024);
     }
   };
-  // weight-row DMA geometry (fixed per lane): instruction j covers rows 8 (wave + 8 j) .. + 7
-  int64_t boff[W3_BPW];
+  // weight DMA: per-lane 32-bit byte offsets (row n * kpad + 16-B piece) from a workgroup-uniform base, so each
+  // instruction is a saddr + voffset access with no per-step 64-bit address arithmetic; instruction j covers rows
+  // 8 (wave + 8 j) .. + 7
+  uint32_t boff[W3_BPW];
 #pragma unroll
   for (int j = 0; j < W3_BPW; ++j) {
     const int n = 8 * (wave + 8 * j) + (lane >> 3);
-    boff[j] = (int64_t)n * P.kpad + ((lane & 7) ^ (n & 7)) * 8;
+    boff[j] = (uint32_t)(n * P.kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
   }
-  // issue cursor: weight step ig = (tile iti, chunk ic, tap itap) -> slot ig % 3
-  int ig = 0, ic = 0, itap = 0, iti = 0, icol0;
+  // issue cursor: weight step ig = (tile iti, chunk ic, tap itap) at element offset iwoff of the weight plane; past
+  // the last step it stays on the last tile (the ring slot it refills is never read again)
+  int ig = 0, ic = 0, itap = 0, iti = 0;
+  int64_t iwoff;
   {
-    int b_, t0_;
-    tile_of(0, b_, t0_, icol0);
+    int b_, t0_, col0_;
+    tile_of(0, b_, t0_, col0_);
+    iwoff = (int64_t)col0_ * P.kpad;
   }
   auto issue_wt = [&](int sl) {
-    const u16* base = P.w + (int64_t)icol0 * P.kpad + itap * Cp + ic * 64;
+    const char* base = reinterpret_cast<const char*>(P.w + iwoff);
 #pragma unroll
     for (int j = 0; j < W3_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 8 * j) * 1024);
-    ++ig;
+  };
+  auto advance_wt = [&]() {
+    if (++ig >= total) return;
+    iwoff += Cp;
     if (++itap == K) {
       itap = 0;
+      iwoff += 64 - (int64_t)K * Cp;
       if (++ic == nC) {
         ic = 0;
-        if (++iti < my_n) {
-          int b_, t0_;
-          tile_of(iti, b_, t0_, icol0);
-        }
+        int b_, t0_, col0_;
+        tile_of(++iti, b_, t0_, col0_);
+        iwoff = (int64_t)col0_ * P.kpad;
       }
     }
   };
@@ -861,87 +861,85 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   // prologue: window 0, weight 0, window 1, weight 1, weight 2 (in this order: the mid-step waits count on it)
   stage_win(0);
   issue_wt(0);
-  int pend = 0;  // vm instructions issued after the ones the next wait needs
-  if (nchunks > 1) {
-    stage_win(1);
-    pend += W3_WPW;
-  }
-  if (total > 1) {
-    issue_wt(1);
-    pend += W3_BPW;
-  }
-  if (total > 2) {
-    issue_wt(2);
-    pend += W3_BPW;
-  }
-  w3_wait_barrier_n(pend);
-  pend = total > 2 ? W3_BPW : 0;  // at step 0's mid wait (for weight 1): weight 2 may stay in flight
+  advance_wt();
+  if (nchunks > 1) stage_win(1);
+  issue_wt(1);
+  advance_wt();
+  issue_wt(2);
+  advance_wt();
+  if (nchunks > 1) w3_wait_barrier<W3_WPW + 2 * W3_BPW>();
+  else w3_wait_barrier<2 * W3_BPW>();
+  bool win_last = false;  // a window DMA was issued at the previous mid-step (it may stay in flight)
 
-  bf16x8 af[TM], bA[TN], bB[TN];
+  bf16x8 aA[TM], aB[TM], bA[TN], bB[TN];  // slice-0 / slice-1 fragments
 #pragma unroll
-  for (int i = 0; i < TM; ++i) af[i] = rdA(0, 0, 0, i);
+  for (int i = 0; i < TM; ++i) aA[i] = rdA(0, 0, 0, i);
 #pragma unroll
   for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
 
   int ti = 0, c = 0, tap = 0, sl = 0, q = 0;  // q: global chunk (window buffer q & 1)
   for (int g = 0; g < total; ++g) {
-    // ---- slice 0: MFMAs on (af, bA); slice 1's B fragments (this slot) and A fragments (row by row) read under them
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
+    // ---- slice 0: MFMAs on (aA, bA); slice 1's fragments (this slot, this window) read under them
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bA[j], acc[i][j]);
-      af[i] = rdA(q & 1, tap, 1, i);
-    }
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
+      if (i == 0) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(q & 1, tap, 1, ii);
+      }
     }
+    // pin the interleave: all ten reads of the next slice's fragments after the first row's MFMAs, so the newest
+    // is 18 MFMAs old when the next slice starts (the compiler's wait there is lgkmcnt(0)); issued before the first
+    // row they would leave 16 LDS reads outstanding, past lgkmcnt's 4-bit range
+    __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
     __builtin_amdgcn_s_setprio(0);
 
     // ---- mid-step: weight step g + 1 (and at a chunk's last step the next chunk's window) resident in every
-    //      wave's share; every wave done reading this slot and, at a chunk's last step, this chunk's window
+    //      wave's share; every wave done reading this slot and, at a chunk's last step, this chunk's window.  Loads
+    //      issued after weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay
+    //      in flight
     const bool chunk_end = tap == K - 1;
-    if (g + 1 < total) w3_wait_barrier_n(pend);
-    pend = 0;
+    if (win_last) w3_wait_barrier<W3_BPW + W3_WPW>();
+    else w3_wait_barrier<W3_BPW>();
+    win_last = false;
     if constexpr (!ab_dma) {
       if (chunk_end && q + 2 < nchunks) {
         stage_win(q + 2);
-        pend += W3_WPW;
-      }
-      if (ig < total) {
-        issue_wt(sl);
-        pend += W3_BPW;
+        win_last = true;
       }
     }
 
-    // ---- slice 1: MFMAs on (af, bB); the next step's slice-0 fragments read under them
+    // ---- slice 1: MFMAs on (aB, bB); the next step's slice-0 fragments read under them
     const int sl1 = sl == 2 ? 0 : sl + 1;
     const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
     const int ntap = chunk_end ? 0 : tap + 1;
     // (after the last step these re-read resident LDS: harmless)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bB[j], acc[i][j]);
-      af[i] = rdA(nbuf, ntap, 0, i);
-    }
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+      if (i == 0) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+        // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
+        if constexpr (!ab_dma) issue_wt(sl);
+      }
     }
+    __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+    if constexpr (!ab_dma) __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (!ab_dma) advance_wt();
 
     sl = sl1;
     if (!chunk_end) {
@@ -1025,6 +1023,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   P.tiles_n = a.N / W3_BN;
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
   if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
+  if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
   P.nwg = (int)nt;
   const int ord = knobs().wconv_order;
   P.n_major = ord >= 0 ? ord : 1;
@@ -1069,7 +1068,12 @@ static bool wconv2_tile256(const alcm_opconv_args& a) {
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
   const int var = knobs().wconv;
-  if (knobs().wconv3 && !actepi && !a.geglu_plane && a.out_stride <= 0 && wconv3_try(a, wplane, flops, bytes, s))
+  // persistent 8-wave kernel (ALCM_WCONV3: -1 by shape, 0 off, 1 wherever eligible): by shape where the 256-row
+  // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %)
+  const int w3 = knobs().wconv3;
+  const int mt256 = (a.T + W3_BM - 1) / W3_BM;
+  if (w3 != 0 && !actepi && !a.geglu_plane && a.out_stride <= 0 && (w3 > 0 || a.T * 100 >= mt256 * W3_BM * 85) &&
+      wconv3_try(a, wplane, flops, bytes, s))
     return 1;
   const bool strided = a.out_stride > 0;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;

@@ -353,7 +353,12 @@ def test_wconv3_persistent(K, C, T, k, dil, grid, prec, monkeypatch):
         acc = dev(torch.ones((B, T, C)))
         return K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
                         accumulate_into=acc).cpu() - 1
-    y2 = run()
+    monkeypatch.setenv("ALCM_WCONV3", "0")
+    _hip.reload_knobs()
+    try:
+        y2 = run()
+    finally:
+        monkeypatch.delenv("ALCM_WCONV3")
     monkeypatch.setenv("ALCM_WCONV3", "1")
     monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
     _hip.reload_knobs()
