@@ -107,6 +107,7 @@ struct Knobs {
                                  // 2 no MFMA, 4 no window DMA)
   int sgemm = 1;                 // ALCM_SGEMM: DiT proj_in / proj_out on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
+  int tconv_stagger = -1;        // ALCM_TCONV_STAGGER: streamed narrow conv grid: -1 by shape, 0 one workgroup per tile, >= 1 persistent (stagger - 1 sleeps)
   int tconv_wgs = 0;             // ALCM_TCONV_WGS: persistent workgroups per CU of tconv_kernel's grid (0 by shape)
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
                                  // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv

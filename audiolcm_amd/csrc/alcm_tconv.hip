@@ -50,6 +50,7 @@ struct TConvDev {
   int wslots;         // 16-B slots per LDS weight row (odd)
   int ablate;         // diagnostics (ALCM_TCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA,
                       // 4 no window DMA
+  int stagger;        // tconv2: s_sleep(127) count before the second half of a persistent grid starts
 };
 
 __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
@@ -299,7 +300,12 @@ __global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TC
   const int K = P.ksize, dil = P.dil;
   const int nslice = P.kd / 32;
   const int E = BM - 2 * ACT_EPI_HALO;
-  const int tile = blockIdx.x;
+  // persistent grid (ALCM_TCONV_STAGGER >= 1): the second half of the workgroups (the second workgroup of each CU)
+  // starts P.stagger sleeps late, so the two workgroups of a CU alternate K loop (MFMA) and Activation1d epilogue
+  // (VALU) instead of running both phases in lockstep
+  if (P.stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
+    for (int i = 0; i < P.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
   const int mt = tile / P.ncg, cg = tile - mt * P.ncg;
   const int n0 = cg * NS;
   const int b = mt / P.tiles_per_batch;
@@ -415,9 +421,11 @@ __global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TC
 #pragma unroll
       for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (sum == 123.f && P.out) P.out[tid] = sum;
-    return;
+    continue;
   }
   tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P);
+  __syncthreads();  // staged-tile reads retired before the next tile's DMA overwrites the region
+  }
 }
 
 // -------------------------------------------------------------------------------------------------- host
@@ -506,19 +514,31 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   void* tok = prof_start(s);
   int rc;
   if (streamed) {
-    if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11>(P, (int)nt, act, a.res, outw, acc_mode, s);
+    // ALCM_TCONV_STAGGER: 0 = one workgroup per tile; >= 1 = persistent, two (BM 128: three) workgroups per CU, the
+    // second half delayed by stagger - 1 sleeps; -1 (default) by shape: C = 96 persistent with 2 sleeps (scripts/
+    // microbench.py tconv, one box: k11 0.547 -> 0.491 ms, k3 0.300 -> 0.301, conv2 + residual 0.732 -> 0.695), C = 24
+    // one workgroup per tile (persistent measured +5..+17 %)
+    int grid2 = (int)nt;
+    const int stg = knobs().tconv_stagger >= 0 ? knobs().tconv_stagger : (C == 96 ? 3 : 0);
+    if (stg > 0) {
+      int dev = 0, ncu = 256;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * (small ? 3 : 2));
+      P.stagger = stg - 1;
+    }
+    if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11>(P, grid2, act, a.res, outw, acc_mode, s);
     else if (small && C == 48) {
-      if (npb == 2) rc = tc2_mode<48, 48, 2, 128, 14>(P, (int)nt, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<48, 48, 1, 128, 14>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc2_mode<48, 48, 2, 128, 14>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<48, 48, 1, 128, 14>(P, grid2, act, a.res, outw, acc_mode, s);
     } else if (small) {
-      if (npb == 2) rc = tc2_mode<24, 24, 2, 128, 7>(P, (int)nt, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 128, 7>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 128, 7>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 128, 7>(P, grid2, act, a.res, outw, acc_mode, s);
     } else if (C == 48) {
-      if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, (int)nt, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<48, 48, 1, 256, 24>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<48, 48, 1, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
     } else {
-      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 12>(P, (int)nt, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 256, 12>(P, (int)nt, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);
     }
   } else {
     // persistent: a multiple of ncg workgroups so a workgroup's column group (blockIdx % ncg) is the same for every
