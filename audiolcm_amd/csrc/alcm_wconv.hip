@@ -750,8 +750,10 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA
-template <int PREC, int AB>
+// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA.  GEGLU: the DiT FFN
+// up-projection's epilogue (new_attention.py:48-55): interleaved columns (2m, 2m+1) = (value m, gate m) ->
+// value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2]
+template <int PREC, int AB, bool GEGLU = false>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   constexpr bool ab_dma = (AB & 4) != 0;
@@ -785,22 +787,38 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     t0 = (mt - b * P.tiles_per_batch) * W3_BM;
     col0 = nt * W3_BN;
   };
-  // window of global chunk q (tile q / nC, channel chunk q % nC) -> buffer q & 1
-  auto stage_win = [&](int q) {
+  // window of global chunk q (tile q / nC, channel chunk q % nC) -> buffer q & 1, as W3_WPW DMA instructions (each
+  // 8 rows x 128 B per wave); win_setup resolves the chunk once, win_piece issues instruction j
+  const u16* wsrc_base = P.a;  // batch b, channel chunk c
+  int wrow0 = 0;               // first window row's time index (t0 - pad)
+  int wbuf = 0;
+  auto win_setup = [&](int q) {
     const int ti = q / nC, c = q - ti * nC;
     int b, t0, col0;
     tile_of(ti, b, t0, col0);
-#pragma unroll
-    for (int j = 0; j < W3_WPW; ++j) {
-      const int row = 8 * (wave + 8 * j) + (lane >> 3);
-      const int ls = (lane & 7) ^ (row & 7);
-      const int ts = t0 - P.pad + row;
-      const bool ok = row < WR && ts >= 0 && ts < P.T;
-      const u16* src = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + c * 64 + ls * 8
-                          : reinterpret_cast<const u16*>(g_wconv_zero);
-      glds16(src, smem + (q & 1) * W3_WBUF + (wave + 8 * j) * 1024);
-    }
+    wsrc_base = P.a + (int64_t)b * P.T * Cp + c * 64;
+    wrow0 = t0 - P.pad;
+    wbuf = q & 1;
   };
+  auto win_piece = [&](int j) {
+    const int row = 8 * (wave + 8 * j) + (lane >> 3);
+    const int ls = (lane & 7) ^ (row & 7);
+    const int ts = wrow0 + row;
+    const bool ok = row < WR && ts >= 0 && ts < P.T;
+    const u16* src = ok ? wsrc_base + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
+    glds16(src, smem + wbuf * W3_WBUF + (wave + 8 * j) * 1024);
+  };
+  auto stage_win = [&](int q) {
+    win_setup(q);
+#pragma unroll
+    for (int j = 0; j < W3_WPW; ++j) win_piece(j);
+  };
+  // the next chunk's window is spread over the current chunk's first K - 2 steps (piece j at tap j % (K - 2)), so
+  // the whole grid's window stream (40 KB per CU per chunk) does not land as one burst that queues the weight DMA
+  // behind it (a burst every 11 steps cost 12 % in scripts/probes/mfma_lds_probe.hip); issued no later than tap
+  // K - 3, every piece is covered by the counted wait at the chunk's last mid-step
+  const int wspread = P.fpipe ? 1 : K - 2;  // ALCM_WCONV3=2 (A/B): the whole window at the chunk's first step
+
   // weight DMA: per-lane 32-bit byte offsets (row n * kpad + 16-B piece) from a workgroup-uniform base, so each
   // instruction is a saddr + voffset access with no per-step 64-bit address arithmetic; instruction j covers rows
   // 8 (wave + 8 j) .. + 7
@@ -858,18 +876,16 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
                                             (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
   };
 
-  // prologue: window 0, weight 0, window 1, weight 1, weight 2 (in this order: the mid-step waits count on it)
+  // prologue: window 0, weights 0, 1, 2 (window 1 is issued in pieces during chunk 0)
   stage_win(0);
   issue_wt(0);
   advance_wt();
-  if (nchunks > 1) stage_win(1);
   issue_wt(1);
   advance_wt();
   issue_wt(2);
   advance_wt();
-  if (nchunks > 1) w3_wait_barrier<W3_WPW + 2 * W3_BPW>();
-  else w3_wait_barrier<2 * W3_BPW>();
-  bool win_last = false;  // a window DMA was issued at the previous mid-step (it may stay in flight)
+  w3_wait_barrier<2 * W3_BPW>();
+  int pieces_last = 0;  // window pieces issued at the previous mid-step (they may stay in flight)
 
   bf16x8 aA[TM], aB[TM], bA[TN], bB[TN];  // slice-0 / slice-1 fragments
 #pragma unroll
@@ -905,13 +921,20 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     //      issued after weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay
     //      in flight
     const bool chunk_end = tap == K - 1;
-    if (win_last) w3_wait_barrier<W3_BPW + W3_WPW>();
-    else w3_wait_barrier<W3_BPW>();
-    win_last = false;
+    switch (pieces_last) {
+      case 0: w3_wait_barrier<W3_BPW>(); break;
+      case 1: w3_wait_barrier<W3_BPW + 1>(); break;
+      case 2: w3_wait_barrier<W3_BPW + 2>(); break;
+      default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
+    }
+    pieces_last = 0;
     if constexpr (!ab_dma) {
-      if (chunk_end && q + 2 < nchunks) {
-        stage_win(q + 2);
-        win_last = true;
+      if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
+        if (tap == 0) win_setup(q + 1);
+        for (int j = tap; j < W3_WPW; j += wspread) {
+          win_piece(j);
+          ++pieces_last;
+        }
       }
     }
 
@@ -950,7 +973,31 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     ++q;
     if (++c == nC) {
       // ---- tile epilogue, straight from the accumulators (fp32 out = (acc + bias + res) * scale (+ out))
-      if constexpr ((AB & 1) == 0) {
+      if constexpr ((AB & 1) == 0 && GEGLU) {
+        int b, t0, col0;
+        tile_of(ti, b, t0, col0);
+        float bv[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
+        // every lane evaluates gelu of its own column (one instruction stream for all lanes); the value lane of a
+        // pair takes the gate's from its neighbour, and lane 4q stores the two outputs of columns 4q .. 4q + 3
+        const int No = P.N / 2;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            u16* orow = P.gplane + ((int64_t)b * P.T + min(t, P.T - 1)) * No + (col0 + wn * 96 + (lane & 15)) / 2;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const float x = acc[i][j][r] + bv[j];
+              const float gx = alcm_act(x, ACT_GELU_ERF);
+              const float y = x * __shfl_xor(gx, 1);
+              const float y2 = __shfl_xor(y, 2);
+              if ((lane & 3) == 0 && t < P.T) op_store2<PREC>(orow + j * 8, 0, f32x2{y, y2});
+            }
+          }
+      } else if constexpr ((AB & 1) == 0) {
         int b, t0, col0;
         tile_of(ti, b, t0, col0);
         float bv[TN];
@@ -999,12 +1046,13 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 
 static int g_ncu = 0;
 
-// Eligible: fp16 / bf16 operands, Cp % 64 == 0, 2 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
+// Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
 // residual, scale, accumulate; no GEGLU / strided / fused activation).  Returns 1 when it launched.
 static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  if (a.out_act || a.geglu_plane || a.out_stride > 0 || a.Cp % 64 || a.ksize < 2 || (a.ksize - 1) * a.dil > 64 ||
-      a.N % W3_BN || !a.out)
+  const bool gl = a.geglu_plane != nullptr;
+  if (a.out_act || a.out_stride > 0 || a.Cp % 64 || a.ksize < 3 || (a.ksize - 1) * a.dil > 64 || a.N % W3_BN ||
+      (!gl && !a.out) || (gl && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))))
     return 0;
   if (!g_ncu) {
     int dev = 0, n = 0;
@@ -1019,6 +1067,8 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+  P.gplane = (u16*)a.geglu_plane;
+  P.fpipe = knobs().wconv3 == 2;  // wconv3: window DMA in one burst instead of spread over the chunk's steps
   P.tiles_per_batch = (a.T + W3_BM - 1) / W3_BM;
   P.tiles_n = a.N / W3_BN;
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
@@ -1039,13 +1089,16 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
 #undef W3AB
       default: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P); break;
     }
+  } else if (gl) {
+    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, true>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, true>), dim3(grid), dim3(512), 0, s, P);
   } else {
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0>), dim3(grid), dim3(512), 0, s, P);
   }
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0>", a.prec);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s>", a.prec, gl ? "true" : "false");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -1069,11 +1122,12 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
               hipStream_t s) {
   const int var = knobs().wconv;
   // persistent 8-wave kernel (ALCM_WCONV3: -1 by shape, 0 off, 1 wherever eligible): by shape where the 256-row
-  // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %)
+  // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %),
+  // not for the GEGLU up-projection (its register epilogue evaluates erf on every lane: 5.25 vs 4.94 ms/step)
   const int w3 = knobs().wconv3;
   const int mt256 = (a.T + W3_BM - 1) / W3_BM;
-  if (w3 != 0 && !actepi && !a.geglu_plane && a.out_stride <= 0 && (w3 > 0 || a.T * 100 >= mt256 * W3_BM * 85) &&
-      wconv3_try(a, wplane, flops, bytes, s))
+  if (w3 != 0 && !actepi && a.out_stride <= 0 &&
+      (w3 > 0 || (a.T * 100 >= mt256 * W3_BM * 85 && !a.geglu_plane)) && wconv3_try(a, wplane, flops, bytes, s))
     return 1;
   const bool strided = a.out_stride > 0;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
   const bool act = actepi != nullptr;
@@ -1111,7 +1165,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     // elsewhere (the N tiles of an M tile share its input window in L2)
     const int tiles_m = a.B * ((a.T + P.tstride - 1) / P.tstride);
     const int ord = knobs().wconv_order;
-    P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && tiles_m >= 128);
+    // (the GEGLU up-projection, 64 M tiles x 48 N tiles of 1 MB weight slices: N-major -4 %, its M-major order
+    // re-reads the weights from the Infinity Cache once per M tile, 3 GB counted per launch)
+    P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && (tiles_m >= 128 || (a.geglu_plane && tiles_m >= 64)));
     P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
     P.tiles_n = a.N / BN2;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;

@@ -53,7 +53,23 @@ __global__ __launch_bounds__(512, 1) void probe(float* out, int steps, const cha
       __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
     }
     __builtin_amdgcn_s_setprio(0);
-    if (V >= 3) {
+    if (V >= 5) {
+      // + the conv's window stream: every 11th step five 1-KB DMA instructions per wave from the 256 MB buffer
+      // into the other window buffer (here: the upper 40 KB of the A region), waited on with the weights
+      if (tap == 10) __builtin_amdgcn_s_waitcnt((8) | (7 << 4));
+      else __builtin_amdgcn_s_waitcnt((3) | (7 << 4));
+      __builtin_amdgcn_s_barrier();
+      if (tap == 0) {
+        const long wb = ((long)blockIdx.x * 40960 * 31 + (long)g * 40960) % (src_bytes - 40960);
+        for (int j = 0; j < 5; ++j)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + wb + (wave + 8 * j) * 1024 + lane * 16),
+                                           (lds_void_t*)(smem + 40960 + (wave + 8 * j) * 1024), 16, 0, 0);
+      }
+      const long base = ((long)g * 24576) % 65536;
+      for (int j = 0; j < 3; ++j)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + base + (wave + 8 * j) * 1024 + lane * 16),
+                                         (lds_void_t*)(smem + 81920 + sl * 24576 + (wave + 8 * j) * 1024), 16, 0, 0);
+    } else if (V >= 3) {
       __builtin_amdgcn_s_waitcnt((3) | (7 << 4));  // vmcnt(3) lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
       const long base = (V == 3 ? ((long)g * 24576) % 65536 : ((long)blockIdx.x * 24576 * 97 + (long)g * 24576) % (src_bytes - 24576));
@@ -117,6 +133,7 @@ int main() {
     run<2>(out, 256, steps, "V2 + lgkmcnt(0) + barrier per step", src, nb);
     run<3>(out, 256, steps, "V3 + 24 KB DMA per step (L2-resident)", src, nb);
     run<4>(out, 256, steps, "V4 + 24 KB DMA per step (streamed)", src, nb);
+    run<5>(out, 256, steps, "V5 V3 + 40 KB streamed window per 11 steps", src, nb);
   }
   return 0;
 }

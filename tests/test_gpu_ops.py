@@ -372,6 +372,34 @@ def test_wconv3_persistent(K, C, T, k, dil, grid, prec, monkeypatch):
     assert rel_l2(y3.numpy(), y2.numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("T,prec", [(467, 2), (467, 0), (300, 2)])
+def test_wconv3_geglu_plane(K, T, prec, monkeypatch):
+    """DiT Conv1dFeedForward up-projection (k9, GEGLU, new_attention.py:48-55) on the persistent wide conv (opt-in
+    there): the GEGLU plane from the accumulators (lane-pair exchange) agrees with the two-workgroup kernel's
+    LDS-staged epilogue to the plane's rounding (same products and summation order; the gelu's instruction
+    contraction differs, so single elements may round to the neighbouring fp16 / bf16 value), and matches the fp32
+    reference within the plane tolerance."""
+    from audiolcm_amd import _hip
+    B, C, N, k = 2, 576, 4608, 9
+    x = _r((B, T, C), 95)
+    w, bias = _r((N, C, k), 96, 1.0 / np.sqrt(C * k)), _r((N,), 97, 0.05)
+    pl = K.operand_planes(dev(x), prec)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("ALCM_WCONV3", v)
+        _hip.reload_knobs()
+        try:
+            y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, geglu=True)
+        finally:
+            monkeypatch.delenv("ALCM_WCONV3")
+            _hip.reload_knobs()
+        outs.append((y.view(torch.float16) if prec == 2 else y.view(torch.bfloat16)).float().cpu()[0])
+    assert rel_l2(outs[1].numpy(), outs[0].numpy()) < (1e-3 if prec == 0 else 1e-4)
+    h = F.conv1d(x.permute(0, 2, 1), w, bias, padding=(k - 1) // 2).permute(0, 2, 1)
+    ref = h[..., 0::2] * F.gelu(h[..., 1::2])
+    assert rel_l2(outs[1].numpy(), ref.numpy()) < TOL[prec] * 4
+
+
 @pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
                                                  (192, 96, 900, 2, 2), (96, 48, 333, 2, 0)])
 def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
