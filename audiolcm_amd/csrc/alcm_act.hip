@@ -163,6 +163,134 @@ int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* 
   return 0;
 }
 
+// Fused BigVGAN output head (models.py:201-203): activation_post (Activation1d) -> conv_post (k7, C -> 1, zero pad 3)
+// -> tanh, all in fp32 on the VALU, one launch.  Replaces an Activation1d into bf16 hi/lo planes (its 8 B per element
+// written and read back) and a split-precision N = 1 MFMA conv padded to 16 columns (0.32 + 0.74 ms per step).  Per
+// tile of 128 waveform samples of one clip: phase 1 as act_coop_kernel (every upsampled + SnakeBeta sample once,
+// replicate padding by clamped indices, the same tap order), phase 2 the 12-tap down filter for the 134 activation
+// rows the conv reads (rows outside [0, T) are the conv's zero padding) into LDS, phase 3 two lanes per sample (12
+// channels each) for the 7 x C taps, summed in (tap, channel) order per half, bias, tanh.
+template <int C>
+__global__ __launch_bounds__(256) void post_kernel(const float* __restrict__ x, float* __restrict__ wav, int T,
+                                                   const float* __restrict__ aexp, const float* __restrict__ ibeta,
+                                                   const Taps12O f, const float* __restrict__ w, float bias,
+                                                   int tiles_t) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int NP = C / 2;           // channel pairs
+  constexpr int TT = 128;             // samples per tile
+  constexpr int AR = TT + 6;          // activation rows the k7 conv reads
+  constexpr int SEG = 18, NSEG = 16;  // phase 1: 16 segments of 18 upsampled samples (>= 2 AR + 12)
+  constexpr int RS = NP + 1;          // sample-row stride (f32x2)
+  constexpr int RUN = 9;              // phase 2: 16 runs of 9 rows (>= AR)
+  constexpr int ARS = C + 1;          // activation row stride (floats, odd)
+  static_assert(NP <= 16 && NSEG * SEG >= 2 * AR + 12 && 16 * RUN >= AR, "post tile");
+  __shared__ __attribute__((aligned(16))) f32x2 sv[NSEG * SEG * RS];
+  __shared__ float av[16 * RUN * ARS];
+  __shared__ float wl[7 * C];
+  const int tid = threadIdx.x;
+  const int tile = blockIdx.x % tiles_t, b = blockIdx.x / tiles_t;
+  const int t0 = tile * TT;
+  const int j0a = t0 - 3;              // first activation row
+  const int m0 = 2 * j0a - 6;          // first upsampled sample (even)
+  for (int i = tid; i < 7 * C; i += 256) wl[i] = w[i];
+  const float* xb = x + (int64_t)b * T * C;
+  const int p = tid & 15;
+  const bool live = p < NP;
+  const int c = 2 * (live ? p : 0);
+  const f32x2 ear = f32x2{aexp[c], aexp[c + 1]} * INV_PI;
+  const f32x2 h = f32x2{ibeta[c], ibeta[c + 1]} * 0.5f;
+  // ---- phase 1: upsampled + SnakeBeta samples m0 + seg * 18 .. + 17 of pair p
+  if (live) {
+    const int seg = tid >> 4;
+    const int mb = m0 + seg * SEG;
+    const int xlo = mb / 2 - 3;
+    if (mb >= 0 && mb + SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1) {
+      f32x2 win[15];
+#pragma unroll
+      for (int i = 0; i < 15; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (xlo + i) * C + c);
+      f32x2 u[SEG];
+#pragma unroll
+      for (int q = 0; q < SEG; ++q) u[q] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+        for (int q = 0; q < SEG; ++q) {
+          const int ku = 2 * kk + ((q & 1) ? 0 : 1);
+          u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
+        }
+#pragma unroll
+      for (int q = 0; q < SEG; ++q) sv[(seg * SEG + q) * RS + p] = snake2(u[q], ear, h);
+    } else {
+      for (int q = 0; q < SEG; ++q) {
+        int m = mb + q;
+        m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+        f32x2 u = f32x2{0.f, 0.f};
+        for (int kk = 0; kk < 6; ++kk) {
+          const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+          int xi = (m + 5 - ku) / 2;
+          xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+          u = fma2(f32x2{f.up[ku], f.up[ku]}, *reinterpret_cast<const f32x2*>(xb + xi * C + c), u);
+        }
+        sv[(seg * SEG + q) * RS + p] = snake2(u, ear, h);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: activation rows j0a + run * 9 .. + 8 of pair p: o[r] = sum_k dn[k] * sv[2 (row) + 1 + k]
+  const int run = tid >> 4;
+  const int r0 = run * RUN;
+  if (live && r0 < AR) {
+    const f32x2* sp = sv + (2 * r0 + 1) * RS + p;
+    f32x2 sm[2 * RUN + 10];
+#pragma unroll
+    for (int i = 0; i < 2 * RUN + 10; ++i) sm[i] = sp[i * RS];
+    f32x2 o[RUN];
+#pragma unroll
+    for (int r = 0; r < RUN; ++r) o[r] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+#pragma unroll
+      for (int r = 0; r < RUN; ++r) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sm[2 * r + k], o[r]);
+#pragma unroll
+    for (int r = 0; r < RUN; ++r) {
+      const int j = j0a + r0 + r;
+      const bool in = j >= 0 && j < T;
+      av[(r0 + r) * ARS + c] = in ? o[r].x : 0.f;
+      av[(r0 + r) * ARS + c + 1] = in ? o[r].y : 0.f;
+    }
+  }
+  __syncthreads();
+  // ---- phase 3: sample t0 + q from activation rows q .. q + 6 (local), lanes 2q / 2q + 1 take channels [0, C/2) /
+  //      [C/2, C)
+  const int q = tid >> 1, half = tid & 1;
+  float acc = 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 7; ++tap)
+#pragma unroll
+    for (int cc = 0; cc < C / 2; ++cc) {
+      const int ch = half * (C / 2) + cc;
+      acc = fmaf(wl[tap * C + ch], av[(q + tap) * ARS + ch], acc);
+    }
+  const float y = acc + __shfl_xor(acc, 1) + bias;
+  const int t = t0 + q;
+  if (half == 0 && t < T) wav[(int64_t)b * T + t] = tanhf(y);
+}
+
+int act_conv_post(const float* x, float* wav, int B, int T, int C, const float* alpha_exp, const float* inv_beta,
+                  const Taps12O& f, const float* w_tc, float bias, hipStream_t s) {
+  if (C != 24) return set_error(ALCM_E_INVALID, "act_conv_post: built for C = 24");
+  if (!x || !wav || !alpha_exp || !inv_beta || !w_tc || B <= 0 || T <= 0 || (((uintptr_t)x) & 7))
+    return set_error(ALCM_E_INVALID, "act_conv_post: bad arguments");
+  if ((int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_conv_post: clip too long");
+  const int tiles_t = (T + 127) / 128;
+  const int64_t nwg = (int64_t)B * tiles_t;
+  if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_conv_post: problem too large");
+  hipLaunchKernelGGL(post_kernel<24>, dim3((unsigned)nwg), dim3(256), 0, s, x, wav, T, alpha_exp, inv_beta, f, w_tc,
+                     bias, tiles_t);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 // fp32 channels-last rows -> MFMA operand planes [rows][Cp] (channels C .. Cp-1 zero), the format `prec` reads:
 // the input of a plane conv whose producer writes fp32 (the BigVGAN upsampler reads the stage output x)
 template <int PREC>

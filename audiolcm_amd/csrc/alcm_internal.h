@@ -46,6 +46,10 @@ int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, co
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
 // fp32 rows [rows][C] -> operand planes [rows][Cp] in the format of `prec` (SPLIT: lo plane rows * Cp after hi)
 int to_planes(const float* x, void* y, int64_t rows, int C, int Cp, int prec, hipStream_t s);
+// BigVGAN output head: Activation1d -> conv_post (k7, C -> 1, weights [tap][C] fp32) -> tanh, fp32 (alcm_act.hip)
+struct Taps12O;
+int act_conv_post(const float* x, float* wav, int B, int T, int C, const float* alpha_exp, const float* inv_beta,
+                  const Taps12O& f, const float* w_tc, float bias, hipStream_t s);
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
@@ -107,6 +111,7 @@ struct Knobs {
                                  // 2 no MFMA, 4 no window DMA)
   int sgemm = 1;                 // ALCM_SGEMM: DiT proj_in / proj_out on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
+  bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)
   int tconv_stagger = -1;        // ALCM_TCONV_STAGGER: streamed narrow conv grid: -1 by shape, 0 one workgroup per tile, >= 1 persistent (stagger - 1 sleeps)
   int tconv_wgs = 0;             // ALCM_TCONV_WGS: persistent workgroups per CU of tconv_kernel's grid (0 by shape)
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,

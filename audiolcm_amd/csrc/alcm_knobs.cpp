@@ -47,6 +47,7 @@ static Knobs read_knobs() {
   k.tconv_wgs = env_int("ALCM_TCONV_WGS", 0);
   k.tconv_bm = env_int("ALCM_TCONV_BM", 256);
   k.tconv_stagger = env_int("ALCM_TCONV_STAGGER", -1);
+  k.post_planes = env_set("ALCM_POST_PLANES");
   k.sgemm = env_int("ALCM_SGEMM", 1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   return k;

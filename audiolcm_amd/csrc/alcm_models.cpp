@@ -127,6 +127,8 @@ struct StageW {
 struct VocW {
   int num_mels = 80, c0 = 1536;
   ConvW pre, post;
+  float* post_w32 = nullptr;  // conv_post weight [tap][C] fp32 (the fused output head, act_conv_post)
+  float post_bias = 0.f;
   std::vector<StageW> st;
   ActW post_act;
 };
@@ -591,8 +593,15 @@ static void build_voc(Ingest& I, const int* ic, int nic) {
   }
   const int ch = G.st.back().cout;
   G.post_act = build_act(I, "activation_post.", ch);
-  G.post.w = I.pack(I.wn("conv_post.", {1, ch, 7}), 1, ch, 7, 0, 1, 0, 32);
-  G.post.b = I.upload(I.get("conv_post.bias", {1}));
+  const std::vector<float> pw = I.wn("conv_post.", {1, ch, 7});
+  G.post.w = I.pack(pw, 1, ch, 7, 0, 1, 0, 32);
+  const std::vector<float> pb = I.get("conv_post.bias", {1});
+  G.post.b = I.upload(pb);
+  std::vector<float> ptc((size_t)7 * ch);
+  for (int c = 0; c < ch; ++c)
+    for (int k = 0; k < 7; ++k) ptc[(size_t)k * ch + c] = pw[(size_t)c * 7 + k];
+  G.post_w32 = I.upload(ptc);
+  G.post_bias = pb[0];
 }
 
 // ------------------------------------------------------------------ launch helpers
@@ -1491,6 +1500,21 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   // conv_post maps 24 channels to the waveform: its input rounding shows up 1:1 in the output, so the
   // mixed policy keeps it bf16x3 (one launch, ~5e-4 of the waveform error budget otherwise)
   const int ppost = m->policy == ALCM_POLICY_BF16 ? PREC_BF16 : PREC_SPLIT;
+  if (ppost == PREC_SPLIT && G.st.back().cout == 24 && G.post_w32 && !knobs().post_planes) {
+    // one fused fp32 launch (alcm_act.hip post_kernel): exact fp32 where the split path approximates it
+    Taps12O f;
+    for (int k = 0; k < 12; ++k) {
+      f.up[k] = 2.0f * G.post_act.fup[k];
+      f.dn[k] = G.post_act.fdn[k];
+    }
+    void* tok = prof_start(s);
+    ALCM_TRY(act_conv_post(x, wav, B, T, 24, G.post_act.aexp, G.post_act.ibeta, f, G.post_w32, G.post_bias, s));
+    if (tok) {
+      const double n = (double)B * T;
+      prof_stop(tok, s, "alcm::post_kernel<24>", n * 24 * (2 * 24 + 2 * 12) + n * 2 * 7 * 24, n * 24 * 4 + n * 4);
+    }
+    return 0;
+  }
   ALCM_TRY(act_planes(s, G.post_act, x, w, B, T, G.st.back().cout, ppost));
   return plane_conv(s, G.post, w, B, T, 1, nullptr, wav, 1.f, 0, ACT_TANH, ppost);
 }

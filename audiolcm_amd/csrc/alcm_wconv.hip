@@ -750,13 +750,14 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA.  GEGLU: the DiT FFN
+// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA, 16 no K-loop waits /
+// barriers.  GEGLU: the DiT FFN
 // up-projection's epilogue (new_attention.py:48-55): interleaved columns (2m, 2m+1) = (value m, gate m) ->
 // value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2]
 template <int PREC, int AB, bool GEGLU = false>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
-  constexpr bool ab_dma = (AB & 4) != 0;
+  constexpr bool ab_dma = (AB & 4) != 0, ab_sync = (AB & 16) != 0;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -921,7 +922,8 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     //      issued after weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay
     //      in flight
     const bool chunk_end = tap == K - 1;
-    switch (pieces_last) {
+    if constexpr (ab_sync) {
+    } else switch (pieces_last) {
       case 0: w3_wait_barrier<W3_BPW>(); break;
       case 1: w3_wait_barrier<W3_BPW + 1>(); break;
       case 2: w3_wait_barrier<W3_BPW + 2>(); break;
@@ -1085,7 +1087,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if (ab && a.prec == PREC_F16) {
     switch (ab) {
 #define W3AB(v) case v: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, v>), dim3(grid), dim3(512), 0, s, P); break;
-      W3AB(1) W3AB(4) W3AB(5)
+      W3AB(1) W3AB(4) W3AB(5) W3AB(21)
 #undef W3AB
       default: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P); break;
     }
