@@ -24,6 +24,7 @@ static Knobs read_knobs() {
   k.wconv_fpipe = env_int("ALCM_WCONV_FPIPE", 1);
   k.wconv3 = env_int("ALCM_WCONV3", -1);
   k.wconv3_grid = env_int("ALCM_WCONV3_GRID", 0);
+  k.w3_epi = env_int("ALCM_W3_EPI", 0);  // 16-B epilogue measured -0.7 % end to end (profiles/r3z)
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;

@@ -750,11 +750,31 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
+// v[r] of lane q of a quad = element (q, r) of a 4 x 4 block -> element (r, q): two DPP butterflies (xor 1, xor 2)
+__device__ __forceinline__ float w3_dpp_xor(float x, int ctrl_is_xor2) {
+  const int i = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, ctrl_is_xor2 ? __builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, true)
+                                                : __builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ void w3_quad_transpose(float (&v)[4], int q) {
+#pragma unroll
+  for (int p = 0; p < 4; p += 2) {
+    const float t = w3_dpp_xor((q & 1) ? v[p] : v[p + 1], 0);
+    if (q & 1) v[p] = t; else v[p + 1] = t;
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float t = w3_dpp_xor((q & 2) ? v[p] : v[p + 2], 1);
+    if (q & 2) v[p] = t; else v[p + 2] = t;
+  }
+}
+
 // AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA, 16 no K-loop waits /
 // barriers.  GEGLU: the DiT FFN
 // up-projection's epilogue (new_attention.py:48-55): interleaved columns (2m, 2m+1) = (value m, gate m) ->
-// value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2]
-template <int PREC, int AB, bool GEGLU = false>
+// value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2].  EPI4: the fp32 epilogue with 16-B
+// accesses after an in-quad transpose (ALCM_W3_EPI=0: the 4-B column-access epilogue, A/B)
+template <int PREC, int AB, bool GEGLU = false, bool EPI4 = true>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   constexpr bool ab_dma = (AB & 4) != 0, ab_sync = (AB & 16) != 0;
@@ -999,6 +1019,37 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
               if ((lane & 3) == 0 && t < P.T) op_store2<PREC>(orow + j * 8, 0, f32x2{y, y2});
             }
           }
+      } else if constexpr ((AB & 1) == 0 && EPI4) {
+        // 4 x 4 transpose inside each lane quad (two DPP butterfly stages): lane q of a quad then owns ROW
+        // 4 (lane >> 4) + q of the fragment at columns (lane & 12) .. + 3, so bias / residual / accumulate / out move
+        // as one 16-B access per lane per fragment instead of four 4-B column accesses (12 -> 3 memory instructions)
+        int b, t0, col0;
+        tile_of(ti, b, t0, col0);
+        const int q = lane & 3;
+        const int cb = col0 + wn * 96 + (lane & 12);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + q;
+          const int64_t ro = ((int64_t)b * P.T + min(t, P.T - 1)) * P.N + cb;
+          float4 rv[TN], pv[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            rv[j] = P.res ? *reinterpret_cast<const float4*>(P.res + ro + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+            pv[j] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + ro + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            w3_quad_transpose(v, q);
+            const float4 bv = P.bias ? *reinterpret_cast<const float4*>(P.bias + cb + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 o;
+            o.x = (v[0] + bv.x + rv[j].x) * P.out_scale + pv[j].x;
+            o.y = (v[1] + bv.y + rv[j].y) * P.out_scale + pv[j].y;
+            o.z = (v[2] + bv.z + rv[j].z) * P.out_scale + pv[j].z;
+            o.w = (v[3] + bv.w + rv[j].w) * P.out_scale + pv[j].w;
+            if (t < P.T) *reinterpret_cast<float4*>(P.out + ro + j * 16) = o;
+          }
+        }
       } else if constexpr ((AB & 1) == 0) {
         int b, t0, col0;
         tile_of(ti, b, t0, col0);
@@ -1094,13 +1145,18 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   } else if (gl) {
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, true>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, true>), dim3(grid), dim3(512), 0, s, P);
-  } else {
+  } else if (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15)) {
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0>), dim3(grid), dim3(512), 0, s, P);
+  } else {
+    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, false, false>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, false, false>), dim3(grid), dim3(512), 0, s, P);
   }
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s>", a.prec, gl ? "true" : "false");
+    const bool e4 = gl || (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15));
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s>", a.prec, gl ? "true" : "false",
+                  e4 ? "true" : "false");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);

@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--extra-configs", type=int, default=1,
                     help="N=1: also time BASELINE configs[3] (C4: B=64, 4 steps + CFG) and configs[4] (C5: B=16, "
                          "30 s decode) and report them beside the headline")
+    ap.add_argument("--components", type=int, default=1,
+                    help="N=1: also time the SURVEY §8(f) components at the configs[1] batch (text encoders, "
+                         "log-mel front-end + Encoder1D), each with its roofline")
     return ap.parse_args()
 
 
@@ -193,6 +196,77 @@ def extra_configs(pipe, a):
     return out
 
 
+def _component_roofline(prof, wall_s: float):
+    """Roofline of one component call from its per-launch HIP events: the path figure (sum over launches of
+    max(F / 2.5 PF, B / 8 TB/s) / wall), the algorithmic MFMA rate over the wall, and the dominant kernel's own
+    fraction of its bound."""
+    from audiolcm_amd import _hip
+    pf, pb = _hip.PEAK_BF16_FLOPS, _hip.PEAK_HBM_BYTES
+    flops = sum(p["flops"] for p in prof)
+    roof_ms = sum(p["roof_ms"] for p in prof)
+    dom = max(prof, key=lambda p: p["total_ms"])
+    sec = dom["total_ms"] / 1e3
+    mfma = dom["flops"] / max(dom["bytes"], 1) > pf / pb
+    frac = dom["flops"] / sec / pf if mfma else dom["bytes"] / sec / pb
+    return dict(path_roofline_frac_build=round(roof_ms / (1e3 * wall_s), 4), t_roof_ms=round(roof_ms, 3),
+                tflop=round(flops / 1e12, 4), achieved_tflops_over_wall=round(flops / wall_s / 1e12, 1),
+                kernel=dom["name"], kernel_bound="mfma" if mfma else "hbm", kernel_frac=round(frac, 4),
+                kernel_share=round(dom["total_ms"] / max(sum(p["total_ms"] for p in prof), 1e-9), 4),
+                launches=sum(p["launches"] for p in prof))
+
+
+def components(a):
+    """SURVEY §8(f) components at the configs[1] batch, timed like the headline (warm-up, synchronise, K calls),
+    then one instrumented call for the roofline: f1 FrozenCLAPFLANEmbedder.encode from token ids (BERT-base +
+    CLAP Projection + T5-v1.1-large, 32 prompts x 77 tokens each; ldm/modules/encoders/modules.py:567-582) and
+    f4 the audio -> latent direction (NAT_mel log-mel of 32 x 159,744 samples + Encoder1D + quant_conv moments;
+    NAT_mel.py:66-85, ldm/models/autoencoder1d.py encode)."""
+    from audiolcm_amd import _hip, recipe
+    from audiolcm_amd.mel import MelNet
+    from audiolcm_amd.models import AutoencoderKL
+    from audiolcm_amd.text_encoder import CLAPT5TextEncoder
+    B, T = a.batch, a.latent_len
+    g = torch.Generator().manual_seed(7)
+    enc = CLAPT5TextEncoder.from_recipe(0, split="mixed")
+    cfg = enc.cfg
+    ids_b = torch.randint(1, cfg.b_vocab, (B, cfg.max_len), generator=g)
+    ids_t = torch.randint(1, cfg.t_vocab, (B, cfg.max_len), generator=g)
+    mel = MelNet()
+    st = dict(recipe.vae_state(0))
+    st.update(recipe.vae_encoder_state(0))
+    vae = AutoencoderKL(split="mixed").load_state_dict(st)
+    wav = (0.1 * torch.randn((B, 2 * T * HOP), generator=g)).cuda()
+
+    def text():
+        enc.encode_ids(ids_b, ids_t)
+
+    def audio_in():
+        vae.encode(mel(wav))
+    out = {}
+    for name, fn, unit, units in (("text_encode", text, "prompts/s", B),
+                                  ("mel_vae_encode", audio_in, "audio-s/s", B * 2 * T * HOP / SR)):
+        for _ in range(max(1, a.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        _hip.profile_begin()
+        fn()
+        torch.cuda.synchronize()
+        prof = _hip.profile_end()
+        out[name] = dict(value=round(units / dt, 2), unit=unit, ms_per_call=round(1e3 * dt, 3),
+                         roofline=_component_roofline(prof, dt),
+                         workload=(f"{B} prompts x {cfg.max_len} tokens per tower, mixed policy (fp16 MFMA on the "
+                                   f"encoder linears and attention, T5 FFN-out bf16x3)" if name == "text_encode" else
+                                   f"{B} clips x {2 * T * HOP} samples -> log-mel 80x{2 * T} -> Encoder1D moments "
+                                   f"20x{T} (mixed policy)"))
+    del enc, vae, mel
+    return out
+
+
 def main():
     a = parse()
     from audiolcm_amd import _hip, recipe
@@ -310,6 +384,9 @@ def main():
     if world == 1 and a.extra_configs:
         log("other configs (C4, C5)")
         line["other_configs"] = extra_configs(pipe, a)
+    if world == 1 and a.components:
+        log("SURVEY §8(f) components (text encoders, mel + Encoder1D)")
+        line["components"] = components(a)
     if world == 1 and a.also_other_mode:
         log("other precision policies")
         for other in ("mixed", "split", "bf16"):

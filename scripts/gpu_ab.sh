@@ -13,7 +13,7 @@ i=0
 for round in $(seq 1 ${ROUNDS:-2}); do
   for v in "$@"; do
     i=$((i+1))
-    env $v ALCM_BENCH_ALL_KERNELS=1 timeout -k 10 300 python -u bench.py --steps 5 --also-other-mode 0 --cpu-baseline 0 --extra-configs 0 > $out/bench_${round}_$i.json 2> $out/bench_${round}_$i.err || exit $?
+    env $v ALCM_BENCH_ALL_KERNELS=1 timeout -k 10 300 python -u bench.py --steps 5 --also-other-mode 0 --cpu-baseline 0 --extra-configs 0 --components 0 > $out/bench_${round}_$i.json 2> $out/bench_${round}_$i.err || exit $?
     echo "$v: $(python -c "import json;d=json.load(open('$out/bench_${round}_$i.json'));print(d['value'], d['ms_per_step'])")" >> $out/ab.txt
   done
 done

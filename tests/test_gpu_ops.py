@@ -372,6 +372,40 @@ def test_wconv3_persistent(K, C, T, k, dil, grid, prec, monkeypatch):
     assert rel_l2(y3.numpy(), y2.numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("C,T,k,res,grid", [(384, 1100, 3, True, 0), (192, 1500, 3, False, 16),
+                                            (768, 600, 11, True, 8), (192, 257, 7, False, 0)])
+def test_wconv3_wide_epilogue(K, C, T, k, res, grid, monkeypatch):
+    """wconv3's fp32 epilogue with 16-B accesses after the in-quad DPP transpose (opt-in ALCM_W3_EPI=1; -0.7 % end to
+    end, profiles/r3z) vs the default 4-B column-access epilogue: same accumulators, same (acc + bias + res) * scale + out order -> bit-identical,
+    including the masked rows of a partial last tile (T % 256 != 0) and the residual-free form."""
+    from audiolcm_amd import _hip
+    B, prec = 2, 2
+    x = _r((B, T, C), 110)
+    w, bias = _r((C, C, k), 111, 0.7 / np.sqrt(C * k)), _r((C,), 112, 0.05)
+    r = dev(_r((B, T, C), 113)) if res else None
+    pl = K.operand_planes(dev(x), prec)
+    outs = []
+    for epi in ("1", "0"):
+        monkeypatch.setenv("ALCM_WCONV3", "1")
+        monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
+        monkeypatch.setenv("ALCM_W3_EPI", epi)
+        _hip.reload_knobs()
+        try:
+            acc = dev(_r((B, T, C), 114))
+            outs.append(K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=r, out_scale=0.5,
+                                 accumulate_into=acc).cpu())
+        finally:
+            for v in ("ALCM_WCONV3", "ALCM_WCONV3_GRID", "ALCM_W3_EPI"):
+                monkeypatch.delenv(v)
+            _hip.reload_knobs()
+    assert torch.equal(outs[0], outs[1])
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias, padding=(k - 1) // 2).permute(0, 2, 1)
+    if res:
+        ref = ref + r.cpu()
+    ref = ref * 0.5 + _r((B, T, C), 114)
+    assert rel_l2(outs[0].numpy(), ref.numpy()) < TOL[prec]
+
+
 @pytest.mark.parametrize("T,prec", [(467, 2), (467, 0), (300, 2)])
 def test_wconv3_geglu_plane(K, T, prec, monkeypatch):
     """DiT Conv1dFeedForward up-projection (k9, GEGLU, new_attention.py:48-55) on the persistent wide conv (opt-in
