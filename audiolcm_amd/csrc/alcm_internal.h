@@ -87,6 +87,7 @@ struct Knobs {
   int wconv_fpipe = 1;           // ALCM_WCONV_FPIPE: wconv2 fragment-pipelined K loop (0 = per-slice read-then-MFMA)
   int wconv3 = -1;               // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip): -1 by shape, 0 off, 1 on
   int w3_epi = 1;                // ALCM_W3_EPI: wconv3 fp32 epilogue with 16-B accesses after an in-quad transpose (0: 4-B column accesses)
+  bool text_gemm = false;        // ALCM_TEXT_GEMM: text encoders' F16 / BF16 linears on the fp32-A GEMM (A/B; default: planes)
   int wconv3_grid = 0;           // ALCM_WCONV3_GRID: cap on wconv3's persistent workgroups (tests; 0 = one per CU)
   int wconv_tile = -1;           // ALCM_WCONV_TILE: wconv2 tile, 0 = 128 x 192, 1 = 256 x 96, -1 = by shape
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width

@@ -40,6 +40,9 @@ int embed_gather(const int64_t* ids, int rows, const float* table, int64_t vocab
 int rms_stats(const float* x, int rows, int C, float eps, float* mean, float* rstd, hipStream_t s);
 int rms_norm(const float* x, int rows, int C, float eps, const float* w, int L, int64_t out_sb, float* out,
              hipStream_t s);
+int rms_norm_plane(const float* x, int rows, int C, float eps, const float* w, void* out, int prec, hipStream_t s);
+int geglu_pairs(const float* y, int64_t rows, int F, float* out, hipStream_t s);
+int geglu_split_planes(const float* y, int64_t rows, int F, void* plane, int64_t lo_off, hipStream_t s);
 int softmax_rows_bias(float* x, int rows, int n, int64_t ld, int L, int heads, const float* bias, int bld,
                       hipStream_t s);
 int i64_to_f32(const int64_t* t, float* o, int n, hipStream_t s);
@@ -1626,6 +1629,8 @@ static void build_text(Ingest& I, const int* ic, int nic) {
 
 struct TextWs {
   float *x, *tmp, *qkv, *S, *O, *inter, *e1, *g, *mean, *rstd;
+  float* wi;  // T5 wi GEMM output before the gated GELU (plane path)
+  u16* pl;    // operand plane of the linears' A (plane path)
 };
 static TextWs plan_text(const TextW& X, Bump& bp, int B, int L) {
   const size_t R = (size_t)B * L;
@@ -1643,6 +1648,8 @@ static TextWs plan_text(const TextW& X, Bump& bp, int B, int L) {
   w.g = bp.take<float>(R * X.p_out);
   w.mean = bp.take<float>(R);
   w.rstd = bp.take<float>(R);
+  w.wi = bp.take<float>(R * 2 * (size_t)X.t_ff);
+  w.pl = bp.take<u16>(R * (size_t)std::max({X.b_inter, 2 * X.t_ff, (int)dmax, (int)inner}));
   return w;
 }
 
@@ -1687,6 +1694,19 @@ static int lin(hipStream_t s, int prec, int R, const float* x, int C, const Conv
   return conv(s, prec, 1, R, View{x, 0, C, 1, R, C}, w, Out{y, 0, w.w.rows, 1, 1, 0}, o);
 }
 
+// the same linear on an F16 / BF16 operand plane (alcm_opconv, k = 1: the wide-layer / plane conv kernels): y (R, N) =
+// plane (R, C) W^T (+ bias) (+ res) with out_act; the plane is written by the caller
+static int plane_lin(hipStream_t s, int prec, int R, const u16* plane, int C, const ConvW& w, float* y,
+                     const float* res, int act, int64_t plane_lo = 0) {
+  if (w.w.cpad != C || w.w.taps != 1) return set_error(ALCM_E_INVALID, "plane_lin: plane width != packed Cin");
+  alcm_opconv_args g;
+  std::memset(&g, 0, sizeof(g));
+  g.a = plane; g.a_lo_off = plane_lo; g.B = 1; g.T = R; g.C = C; g.Cp = C; g.ksize = 1; g.dil = 1; g.pad = 0;
+  g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.N = w.w.rows;
+  g.bias = w.b; g.res = res; g.out = y; g.out_act = act; g.out_scale = 1.f; g.prec = prec;
+  return opconv(g, s);
+}
+
 static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5_ids, float* out, int B, int L,
                        void* ws, size_t wsb, hipStream_t s) {
   const TextW& X = m->text;
@@ -1701,7 +1721,25 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   ALCM_TRY(embed_gather(clap_ids, R, X.b_word, X.b_vocab, H, X.b_pos_type, L, w.x, s));
   ALCM_TRY(layer_norm(w.x, R, H, H, X.b_eps, X.b_emb_ln.g, X.b_emb_ln.b, nullptr, 0, w.x, H, s));
   const int bdh = H / X.b_heads;
+  // F16 / BF16 linears (mixed / bf16 policies) on operand planes and the plane conv kernels: the fp32-A GEMM with
+  // an in-kernel conversion ran the text towers at 0.05 of the MFMA peak (profiles/r3z, bench components)
+  const bool planes = (pl == PREC_F16 || pl == PREC_BF16) && H % 64 == 0 && D % 64 == 0 && TI % 64 == 0 &&
+                      X.b_inter % 64 == 0 && X.t_ff % 64 == 0 && !knobs().text_gemm;
   for (const BertLayerW& Ly : X.bl) {
+    if (planes) {
+      ALCM_TRY(to_planes(w.x, w.pl, R, H, H, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.qkv, w.qkv, nullptr, 0));
+      ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
+      ALCM_TRY(to_planes(w.O, w.pl, R, H, H, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.ao, w.tmp, w.x, 0));
+      ALCM_TRY(layer_norm_plane(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, w.pl, pl, s));
+      ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, nullptr, 0, w.x, H, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.inter, w.inter, nullptr, ACT_GELU_ERF));
+      ALCM_TRY(to_planes(w.inter, w.pl, R, X.b_inter, X.b_inter, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, X.b_inter, Ly.out, w.tmp, w.x, 0));
+      ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln2.g, Ly.ln2.b, nullptr, 0, w.x, H, s));
+      continue;
+    }
     ALCM_TRY(lin(s, pl, R, w.x, H, Ly.qkv, w.qkv, ConvOpts{}));
     ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
     ConvOpts ra;
@@ -1732,6 +1770,27 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   // ---- T5 encoder (v1.1): pre-RMSNorm blocks, unscaled attention + relative position bias, gated-gelu FFN
   ALCM_TRY(embed_gather(t5_ids, R, X.t_emb, X.t_vocab, D, nullptr, L, w.x, s));
   for (const T5BlockW& Bk : X.tb) {
+    if (planes) {
+      ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln0, w.pl, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.qkv, w.qkv, nullptr, 0));
+      ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
+      ALCM_TRY(to_planes(w.O, w.pl, R, TI, TI, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, TI, Bk.o, w.x, w.x, 0));
+      ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln1, w.pl, pl, s));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.wi, w.wi, nullptr, 0));
+      if (ps == PREC_SPLIT) {
+        // wo on bf16 hi / lo planes of the gated-GELU product (fp32 range, bf16x3 products; see below)
+        const int64_t lo = (int64_t)R * X.t_ff;
+        ALCM_TRY(geglu_split_planes(w.wi, R, X.t_ff, w.pl, lo, s));
+        ALCM_TRY(plane_lin(s, PREC_SPLIT, R, w.pl, X.t_ff, Bk.wo, w.x, w.x, 0, lo));
+      } else {
+        ALCM_TRY(geglu_pairs(w.wi, R, X.t_ff, w.inter, s));
+        ConvOpts r2;
+        r2.res = Res{w.x, 0, D, 1};
+        ALCM_TRY(lin(s, ps, R, w.inter, X.t_ff, Bk.wo, w.x, r2));
+      }
+      continue;
+    }
     ALCM_TRY(rms_stats(w.x, R, D, X.t_eps, w.mean, w.rstd, s));
     ConvOpts oq;
     oq.pro = Pro{Bk.ln0, X.zeros, 0, w.mean, w.rstd, 0};

@@ -85,6 +85,84 @@ int rms_norm(const float* x, int rows, int C, float eps, const float* w, int L, 
   return 0;
 }
 
+// T5LayerNorm straight into an MFMA operand plane (F16 / BF16, [rows][C]): the A operand of the following
+// q/k/v or wi projection on the plane conv (alcm_opconv), instead of an fp32 prologue inside the GEMM
+template <int PREC>
+__global__ __launch_bounds__(256) void rms_plane_kernel(const float* __restrict__ x, int rows, int C, float eps,
+                                                        const float* __restrict__ w, u16* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c] * xr[c];
+  const float r = 1.0f / sqrtf(wave_sum(s) / (float)C + eps);
+  u16* o = out + (int64_t)row * C;
+  for (int c = 2 * lane; c < C; c += 128) {
+    const float a = w[c] * (xr[c] * r), b = w[c + 1] * (xr[c + 1] * r);
+    if constexpr (PREC == PREC_F16) {
+      o[c] = __builtin_bit_cast(u16, (_Float16)a);
+      o[c + 1] = __builtin_bit_cast(u16, (_Float16)b);
+    } else {
+      o[c] = __builtin_bit_cast(u16, (__bf16)a);
+      o[c + 1] = __builtin_bit_cast(u16, (__bf16)b);
+    }
+  }
+}
+
+int rms_norm_plane(const float* x, int rows, int C, float eps, const float* w, void* out, int prec, hipStream_t s) {
+  if (!x || !w || !out || rows <= 0 || C <= 0 || C % 2 || (prec != PREC_F16 && prec != PREC_BF16))
+    return set_error(ALCM_E_INVALID, "rms_norm_plane: bad arguments");
+  if (prec == PREC_F16)
+    hipLaunchKernelGGL(rms_plane_kernel<PREC_F16>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, eps, w, (u16*)out);
+  else
+    hipLaunchKernelGGL(rms_plane_kernel<PREC_BF16>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, eps, w, (u16*)out);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+// T5 gated-GELU from the interleaved wi GEMM output y [rows][2F] (column 2j = wi_1 j, column 2j + 1 = wi_0 j):
+// out [rows][F] = y_2j * gelu_tanh(y_2j+1) — the same expression as the GEMM's geglu == 2 epilogue
+__global__ __launch_bounds__(256) void geglu_pairs_kernel(const float2* __restrict__ y, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float2 v = y[i];
+  out[i] = v.x * alcm_act(v.y, ACT_GELU_TANH);
+}
+
+// the same product written as bf16 hi / lo operand planes (hi = bf16(v), lo = bf16(v - hi); lo plane lo_off
+// elements after hi): the A operand of the bf16x3 wo projection, which needs the fp32 range (T5 v1.1 FFN
+// activations exceed fp16 on real weights)
+__global__ __launch_bounds__(256) void geglu_split_kernel(const float2* __restrict__ y, int64_t n, u16* __restrict__ hi,
+                                                          int64_t lo_off) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float2 v = y[i];
+  const float p = v.x * alcm_act(v.y, ACT_GELU_TANH);
+  const __bf16 h = (__bf16)p;
+  hi[i] = __builtin_bit_cast(u16, h);
+  hi[i + lo_off] = __builtin_bit_cast(u16, (__bf16)(p - (float)h));
+}
+
+int geglu_split_planes(const float* y, int64_t rows, int F, void* plane, int64_t lo_off, hipStream_t s) {
+  if (!y || !plane || rows <= 0 || F <= 0 || lo_off < rows * F || (((uintptr_t)y) & 7))
+    return set_error(ALCM_E_INVALID, "geglu_split_planes: bad arguments");
+  const int64_t n = rows * F;
+  hipLaunchKernelGGL(geglu_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float2*>(y), n, (u16*)plane, lo_off);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
+int geglu_pairs(const float* y, int64_t rows, int F, float* out, hipStream_t s) {
+  if (!y || !out || rows <= 0 || F <= 0 || (((uintptr_t)y) & 7)) return set_error(ALCM_E_INVALID, "geglu_pairs: bad arguments");
+  const int64_t n = rows * F;
+  hipLaunchKernelGGL(geglu_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float2*>(y), n, out);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 // In-place row softmax over scores S[z][i][0..n) (row stride ld) with an additive per-head bias
 // bias[(h * bld + i) * bld + j], h = z % heads (T5Attention: scores += position_bias, then softmax in fp32);
 // zeroes the K padding [n, ld) that the P.V GEMM reads.

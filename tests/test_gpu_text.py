@@ -126,3 +126,36 @@ def test_embedder_encode_captions(enc):
 def states_text():
     from audiolcm_amd import recipe
     return recipe.text_state(0)
+
+
+@pytest.mark.parametrize("scaled", [False, True])
+def test_text_encode_planes_path(scaled, monkeypatch):
+    """ALCM_TEXT_PLANES=1: the F16 linears on operand planes (to_planes / LayerNorm-plane / RMSNorm-plane + the plane
+    conv kernels, k = 1), T5 wi -> fp32 -> gated GELU written as bf16 hi/lo planes -> bf16x3 wo.  Mixed policy
+    within its 3e-3 of the reference-pinned oracle, also with the T5 FFN scaled past the fp16 range (as above)."""
+    from audiolcm_amd import _hip, recipe
+    from audiolcm_amd.text_encoder import CLAPT5TextEncoder
+    from oracle import alcm_oracle as O
+    W = dict(recipe.text_state(0))
+    if scaled:
+        for k in list(W):
+            if ".DenseReluDense.wi_" in k:
+                W[k] = W[k] * 150.0
+            elif ".DenseReluDense.wo." in k:
+                W[k] = W[k] / (150.0 * 150.0)
+    g = golden("text_B2_L77.npz")
+    a, b = torch.from_numpy(g["clap_ids"]), torch.from_numpy(g["t5_ids"])
+    with torch.no_grad():
+        ref = O.text_encode(W, a, b).numpy()
+    monkeypatch.setenv("ALCM_TEXT_PLANES", "1")
+    _hip.reload_knobs()
+    try:
+        m = CLAPT5TextEncoder(split="mixed").load_state_dict(W)
+        out = m.encode_ids(a, b).cpu().numpy()
+    finally:
+        monkeypatch.delenv("ALCM_TEXT_PLANES")
+        _hip.reload_knobs()
+    assert np.isfinite(out).all()
+    err = rel_l2(out, ref)
+    print(f"text planes mixed (scaled={scaled}): {err:.2e}")
+    assert err < 3e-3
