@@ -129,10 +129,11 @@ def states_text():
 
 
 @pytest.mark.parametrize("scaled", [False, True])
-def test_text_encode_planes_path(scaled, monkeypatch):
-    """ALCM_TEXT_PLANES=1: the F16 linears on operand planes (to_planes / LayerNorm-plane / RMSNorm-plane + the plane
-    conv kernels, k = 1), T5 wi -> fp32 -> gated GELU written as bf16 hi/lo planes -> bf16x3 wo.  Mixed policy
-    within its 3e-3 of the reference-pinned oracle, also with the T5 FFN scaled past the fp16 range (as above)."""
+def test_text_encode_gemm_path(scaled, monkeypatch):
+    """The mixed-policy tests above run the default plane path (F16 linears on operand planes: to_planes /
+    LayerNorm-plane / RMSNorm-plane + the plane conv kernels; T5 gated GELU written as bf16 hi/lo planes for a
+    bf16x3 wo).  ALCM_TEXT_GEMM=1 keeps the fp32-A GEMM path (A/B, profiles/r3f): it stays within the same 3e-3 of
+    the reference-pinned oracle, also with the T5 FFN scaled past the fp16 range."""
     from audiolcm_amd import _hip, recipe
     from audiolcm_amd.text_encoder import CLAPT5TextEncoder
     from oracle import alcm_oracle as O
@@ -147,15 +148,15 @@ def test_text_encode_planes_path(scaled, monkeypatch):
     a, b = torch.from_numpy(g["clap_ids"]), torch.from_numpy(g["t5_ids"])
     with torch.no_grad():
         ref = O.text_encode(W, a, b).numpy()
-    monkeypatch.setenv("ALCM_TEXT_PLANES", "1")
+    monkeypatch.setenv("ALCM_TEXT_GEMM", "1")
     _hip.reload_knobs()
     try:
         m = CLAPT5TextEncoder(split="mixed").load_state_dict(W)
         out = m.encode_ids(a, b).cpu().numpy()
     finally:
-        monkeypatch.delenv("ALCM_TEXT_PLANES")
+        monkeypatch.delenv("ALCM_TEXT_GEMM")
         _hip.reload_knobs()
     assert np.isfinite(out).all()
     err = rel_l2(out, ref)
-    print(f"text planes mixed (scaled={scaled}): {err:.2e}")
+    print(f"text gemm path mixed (scaled={scaled}): {err:.2e}")
     assert err < 3e-3
