@@ -304,6 +304,30 @@ def test_opconv(K, C, T, k, dil, prec):
     assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
 
 
+@pytest.mark.parametrize("prec", [1, 2, 0])
+def test_opconv_underfilled_wide_n(K, prec, monkeypatch):
+    """ALCM_OPCONV_TILE=3: N % 128 == 0 problems with fewer 128 x 128 tiles than CUs (the text encoders' N = 1024
+    projections) take the 96-column tiles (a partial last column tile at N = 1024): vs F.conv1d, and vs the default
+    128 x 128 tiles on the same planes (same products and K order: bit-identical)."""
+    from audiolcm_amd import _hip
+    B, T, C, N = 1, 300, 256, 1024
+    x = _r((B, T, C), 120)
+    w, bias = _r((N, C, 1), 121, 1.0 / np.sqrt(C)), _r((N,), 122, 0.05)
+    r = _r((B, T, N), 123)
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias).permute(0, 2, 1) + r
+    pl = K.operand_planes(dev(x), prec)
+    y0 = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    monkeypatch.setenv("ALCM_OPCONV_TILE", "3")
+    _hip.reload_knobs()
+    try:
+        y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    finally:
+        monkeypatch.delenv("ALCM_OPCONV_TILE")
+        _hip.reload_knobs()
+    assert rel_l2(y.numpy(), ref.numpy()) < (3e-5 if prec == 1 else TOL[prec])
+    assert torch.equal(y, y0)
+
+
 @pytest.mark.parametrize("C,T,k,dil", [(768, 600, 11, 5), (384, 1100, 7, 3), (192, 1500, 3, 1), (256, 700, 5, 2),
                                        (384, 520, 11, 1)])
 @pytest.mark.parametrize("prec", [0, 2])
