@@ -726,9 +726,10 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   // one tap per K step (two taps per step measured slower: the larger weight buffers cost occupancy)
   //                                                      BM   BN  WGM WGN TPS
   // small problems whose 128 x 128 tiles would leave CUs idle (the text encoders' N = 1024 projections at
-  // M = 2464: 160 tiles for 256 CUs) take the 96-column tiles (220 tiles) under ALCM_OPCONV_TILE=3 (opt-in, A/B)
+  // M = 2464: 160 tiles for 256 CUs) take the 96-column tiles (220 tiles): text encode 13.5 -> 13.2 ms per B = 32
+  // (profiles/r3v); ALCM_OPCONV_TILE=-1 keeps the 128 x 128 tiles (A/B)
   const int64_t tiles128 = (int64_t)a.B * ((a.T + 127) / 128) * ((N + 127) / 128);
-  const bool underfill = !act && N % 128 == 0 && N > 96 && tiles128 < 256 && knobs().opconv_tile == 3;
+  const bool underfill = !act && N % 128 == 0 && N > 96 && tiles128 < 256 && knobs().opconv_tile != -1;
   int rc;
   if (act && N > 96) rc = set_error(ALCM_E_INVALID, "opconv: fused activation on N > 96 needs the wide kernel");
   else if (N % 192 == 0 && N % 128 != 0) rc = launch_opconv<128, 192, 2, 2, 1>(P, a.B, a.prec, act, flops, bytes, s);

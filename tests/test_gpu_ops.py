@@ -306,9 +306,9 @@ def test_opconv(K, C, T, k, dil, prec):
 
 @pytest.mark.parametrize("prec", [1, 2, 0])
 def test_opconv_underfilled_wide_n(K, prec, monkeypatch):
-    """ALCM_OPCONV_TILE=3: N % 128 == 0 problems with fewer 128 x 128 tiles than CUs (the text encoders' N = 1024
-    projections) take the 96-column tiles (a partial last column tile at N = 1024): vs F.conv1d, and vs the default
-    128 x 128 tiles on the same planes (same products and K order: bit-identical)."""
+    """N % 128 == 0 problems with fewer 128 x 128 tiles than CUs (the text encoders' N = 1024 projections) take the
+    96-column tiles by default (a partial last column tile at N = 1024): vs F.conv1d, and vs the 128 x 128 tiles
+    (ALCM_OPCONV_TILE=-1) on the same planes (same products and K order: bit-identical)."""
     from audiolcm_amd import _hip
     B, T, C, N = 1, 300, 256, 1024
     x = _r((B, T, C), 120)
@@ -316,11 +316,11 @@ def test_opconv_underfilled_wide_n(K, prec, monkeypatch):
     r = _r((B, T, N), 123)
     ref = F.conv1d(x.permute(0, 2, 1), w, bias).permute(0, 2, 1) + r
     pl = K.operand_planes(dev(x), prec)
-    y0 = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
-    monkeypatch.setenv("ALCM_OPCONV_TILE", "3")
+    y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    monkeypatch.setenv("ALCM_OPCONV_TILE", "-1")
     _hip.reload_knobs()
     try:
-        y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+        y0 = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
     finally:
         monkeypatch.delenv("ALCM_OPCONV_TILE")
         _hip.reload_knobs()
