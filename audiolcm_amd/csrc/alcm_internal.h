@@ -71,6 +71,14 @@ struct ActEpiDev;
 int tconv(const alcm_opconv_args& a, const unsigned short* wd, int64_t wd_lo, int kd, const ActEpiDev* act,
           double flops, double bytes, hipStream_t s);
 
+// fused AMPBlock1 half-layer pair of the narrow stages (alcm_ampair.hip): act1 -> conv1 -> act2 -> conv2 + x
+bool ampair_supported(int prec, int C, int ksize, int dil);
+struct Taps12O;
+int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, const unsigned short* w1,
+           const unsigned short* w2, int64_t w_lo, int kd, const float* b1, const float* b2, float out_scale,
+           int accumulate, bool last, const float* ae1, const float* ib1, const Taps12O& f1, const float* ae2,
+           const float* ib2, const Taps12O& f2, int prec, hipStream_t s);
+
 // bf16x3 1x1 conv on split operand planes (alcm_sgemm.hip)
 bool sgemm_planes_ok(int K, int N, int kpad);
 int sgemm_planes(const unsigned short* a, int64_t a_lo, int M, int K, const unsigned short* w, int64_t w_lo, int kpad,
@@ -119,6 +127,9 @@ struct Knobs {
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
                                  // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv
   int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
+  int ampair = 1;                // ALCM_AMPAIR: BigVGAN stages 3-5 as fused AMPBlock half-layer pairs (alcm_ampair.hip),
+                                 // 0 = one launch per Activation1d / conv (tconv)
+  int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
 };
 const Knobs& knobs();
 

@@ -1344,6 +1344,36 @@ static bool stage_tconv(const StageW& S, int prec) {
   return true;
 }
 
+// the narrow stages' AMPBlock half-layer pairs as one fused launch each (alcm_ampair.hip): every pair of the stage
+// or none
+static bool stage_ampair(const StageW& S, int prec) {
+  if (S.rb.empty() || !S.rb[0].c1[0].dw.p) return false;
+  for (const AmpW& A : S.rb)
+    for (size_t l = 0; l < A.dil.size(); ++l)
+      if (!ampair_supported(prec, S.cout, A.k, A.dil[l]) || A.act.size() < 2 * A.dil.size()) return false;
+  return true;
+}
+
+// x_next = x + c2(a2(c1(a1(x)))) of half-layer pair l of resblock A (models.py:72-81); last: the resblock's output
+// times out_scale added into (accumulate) or written to `out` (the stage mean, models.py:190-199)
+static int amp_pair(hipStream_t s, const AmpW& A, size_t l, const float* x, float* out, int B, int T, int C,
+                    float out_scale, int accumulate, bool last, int prec) {
+  const ActW& a1 = A.act[2 * l];
+  const ActW& a2 = A.act[2 * l + 1];
+  Taps12O f1, f2;
+  for (int k = 0; k < 12; ++k) {
+    f1.up[k] = 2.0f * a1.fup[k];  // UpSample1d's ratio-2 gain folded in (resample.py:30)
+    f1.dn[k] = a1.fdn[k];
+    f2.up[k] = 2.0f * a2.fup[k];
+    f2.dn[k] = a2.fdn[k];
+  }
+  const Packed& d1 = A.c1[l].dw;
+  const Packed& d2 = A.c2[l].dw;
+  if (d1.lo != d2.lo || d1.kpad != d2.kpad) return set_error(ALCM_E_INVALID, "amp_pair: weight layouts differ");
+  return ampair(x, out, B, T, C, A.k, A.dil[l], d1.p + 2 * d1.lo, d2.p + 2 * d2.lo, d1.lo, d1.kpad, A.c1[l].b,
+                A.c2[l].b, out_scale, accumulate, last, a1.aexp, a1.ibeta, f1, a2.aexp, a2.ibeta, f2, prec, s);
+}
+
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
                       float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
                       const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false) {
@@ -1456,6 +1486,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const float inv = 1.0f / (float)S.rb.size();
     const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
     const bool dense = fuse && stage_tconv(S, pamp);
+    const bool pair = dense && stage_ampair(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
     if (conc) {  // chains start after the upsampler wrote u
@@ -1472,7 +1503,14 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
         const bool last = l + 1 == A.dil.size();
         // the mean over resblocks accumulates into x: the chains' last convs run in order (j-1 before j)
         if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, ax->ev[j], 0));
-        if (fuse) {
+        if (pair) {
+          ALCM_TRY(amp_pair(sj, A, l, cur, last ? x : nxt, B, To, S.cout, last ? inv : 1.f, last && j > 0, last,
+                            pamp));
+          if (!last) {
+            cur = nxt;
+            nxt = nxt == cb.rb ? cb.t : cb.rb;
+          }
+        } else if (fuse) {
           if (l == 0) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
                               &A.act[2 * l + 1], cb.pl2, dense));

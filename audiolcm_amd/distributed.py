@@ -25,17 +25,20 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def init_from_env(backend: Optional[str] = None, device: Optional[int] = None) -> Tuple[int, int, int]:
+def init_from_env(backend: Optional[str] = None, device: Optional[int] = None,
+                  force: bool = False) -> Tuple[int, int, int]:
     """torch.distributed init from RANK/WORLD_SIZE/LOCAL_RANK (torchrun); returns (rank, world, local).
 
     ``device``: the GPU this rank drives.  It is made current BEFORE the process group exists and, for
-    nccl (RCCL), bound to the group (``device_id``), so collectives and barriers never guess a device."""
+    nccl (RCCL), bound to the group (``device_id``), so collectives and barriers never guess a device.
+    ``force``: create the group even at world 1 (the one-GPU rehearsal of the N>1 code path: every collective
+    below then really runs, over RCCL with backend nccl)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if device is not None:
         torch.cuda.set_device(device)
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
         backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
@@ -65,20 +68,30 @@ def all_reduce_max(value: float, group=None) -> float:
 def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """Gather per-rank row blocks (contiguous shards of n_total rows) into the full (n_total, ...) tensor.
 
-    Shards are padded to the largest shard so a single all_gather_into_tensor moves everything."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1:
+    One all_gather_into_tensor moves everything.  Equal shards (the bench: B prompts per rank) gather straight
+    into the result; ragged ones are padded to the largest shard and compacted afterwards.  Runs whenever a
+    process group exists, world 1 included (the one-GPU RCCL rehearsal); without one it returns ``local``."""
+    if not dist.is_initialized():
         return local
+    world = dist.get_world_size(group)
+    lo, hi = shard_range(n_total, dist.get_rank(group), world)
+    if local.shape[0] != hi - lo:
+        raise ValueError(f"all_gather_rows: local shard has {local.shape[0]} rows, expected {hi - lo}")
     per = -(-n_total // world)
-    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
+    even = per * world == n_total
+    src = local.contiguous()
+    if not even:
+        src = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        src[: local.shape[0]] = local
     out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     if local.is_cuda and dist.get_backend(group) != "nccl":  # gloo (device-map rehearsals): through the host
         host = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_gather_into_tensor(host, pad.cpu(), group=group)
+        dist.all_gather_into_tensor(host, src.cpu(), group=group)
         out.copy_(host)
     else:
-        dist.all_gather_into_tensor(out, pad, group=group)
+        dist.all_gather_into_tensor(out, src, group=group)
+    if even:
+        return out
     rows = [out[r * per: r * per + (shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0])]
             for r in range(world)]
     return torch.cat(rows, 0)

@@ -140,7 +140,7 @@ def summary(layers: List[Layer]) -> dict:
     hb = [l for l in layers if l.bytes / PEAK_HBM > l.flops / PEAK_MFMA]
     return dict(gflop=f / 1e9, gbytes=b / 1e9, t_roof_ms=t * 1e3, mfma_only_ms=f / PEAK_MFMA * 1e3,
                 hbm_only_ms=b / PEAK_HBM * 1e3, hbm_bound_layers=len(hb), layers=len(layers),
-                hbm_bound_t_ms=sum(l.t for l in hb) * 1e3)
+                hbm_bound_t_ms=sum(l.t for l in hb) * 1e3, hbm_bound_gbytes=sum(l.bytes for l in hb) / 1e9)
 
 
 CONFIGS = {

@@ -20,7 +20,8 @@ from conftest import REPO
 
 pytestmark = pytest.mark.gpu
 
-ARGS = ["--steps", "1", "--warmup", "0", "--also-other-mode", "0", "--cpu-baseline", "0", "--extra-configs", "0"]
+ARGS = ["--steps", "1", "--warmup", "0", "--also-other-mode", "0", "--cpu-baseline", "0", "--extra-configs", "0",
+        "--components", "0"]
 
 
 def _run(cmd, tmp_path, name):
@@ -50,3 +51,26 @@ def test_bench_world2_gathers_bit_identical_waveforms(tmp_path):
     assert w1.shape == w2.shape == (64, 159744)
     assert np.isfinite(w1).all() and np.abs(w1).max() > 0
     assert np.array_equal(w1, w2)
+
+
+def test_bench_rccl_world1_collectives(tmp_path):
+    """The RCCL lines of the N>1 path on the one leased GPU: torchrun world 1 with --force-collective runs
+    init_process_group("nccl", device_id), barrier(device_ids), the device all_reduce of the step time and the
+    device all_gather_into_tensor of the waveforms (distributed.py) — the code the driver's 8-GPU job runs — and the
+    gathered waveforms must be bit-identical to the plain one-process run."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    bench = os.path.join(REPO, "bench.py")
+    one = _run([sys.executable, bench, "--gpus", "1", "--batch", "32", "--dump-wav", str(tmp_path / "w1.npy")]
+               + ARGS, tmp_path, "plain")
+    rc = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+               "--master-addr=127.0.0.1", "--master-port=29587", bench, "--gpus", "1", "--batch", "32",
+               "--dist-backend", "nccl", "--force-collective", "1", "--dump-wav", str(tmp_path / "wr.npy")] + ARGS,
+              tmp_path, "rccl")
+    log = open(tmp_path / "rccl.log").read()
+    assert rc["n_gpus"] == 1 and rc["value"] > 0 and one["config"]["global_batch"] == 32
+    assert rc["config"]["dist_backend"] == "nccl" and one["config"]["dist_backend"] is None
+    w1, wr = np.load(tmp_path / "w1.npy"), np.load(tmp_path / "wr.npy")
+    assert w1.shape == wr.shape == (32, 159744)
+    assert np.array_equal(w1, wr), log[-3000:]

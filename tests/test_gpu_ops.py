@@ -594,3 +594,49 @@ def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_ref)
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_d, dense=True)
         assert rel_l2(o_d.cpu().numpy(), o_ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("C,T,k,dil,prec,grid", [(24, 1000, 11, 5, 3, 0), (48, 700, 7, 3, 3, 0), (96, 500, 3, 1, 2, 0),
+                                                 (96, 333, 11, 5, 2, 0), (96, 600, 7, 3, 2, 0), (24, 37, 3, 1, 3, 0),
+                                                 (48, 2000, 11, 5, 3, 8), (24, 5000, 7, 1, 3, 8), (96, 1300, 11, 1, 2, 16)])
+@pytest.mark.parametrize("mode", ["state", "last"])
+def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, monkeypatch):
+    """One AMPBlock1 half-layer pair in one launch (alcm_ampblock_pair, vocoder/bigvgan/models.py:72-81) == the unfused
+    chain it replaces: Activation1d -> operand planes, dense conv1 with the fused Activation1d epilogue, dense conv2 +
+    residual (alcm_opconv_dense) — the same dense K slices, MFMA lanes and Activation1d chains, so bit-identical — incl.
+    the sequence ends (replicate / zero padding), partial last tiles and several tiles per workgroup
+    (ALCM_AMPAIR_GRID); 'last' = a resblock's last pair: (x + ...) * out_scale added into the stage accumulator."""
+    from audiolcm_amd import _hip
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B = 2
+    x = dev(_r((B, T, C), 130))
+    w1, b1 = dev(_r((C, C, k), 131, 0.7 / np.sqrt(C * k))), dev(_r((C,), 132, 0.05))
+    w2, b2 = dev(_r((C, C, k), 133, 0.7 / np.sqrt(C * k))), dev(_r((C,), 134, 0.05))
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    act1 = (dev(_r((C,), 135, 0.3)), dev(_r((C,), 136, 0.3)), f, f)
+    act2 = (dev(_r((C,), 137, 0.3)), dev(_r((C,), 138, 0.3)), f, f)
+    pl1 = K.activation1d_op(x, *act1, prec)
+    _, pl2 = K.opconv(pl1, C, w1, b1, dil, prec, act=act2, fp32_out=False, dense=True)
+    if mode == "state":
+        ref = K.opconv(pl2, C, w2, b2, 1, prec, residual=x, dense=True)
+    else:
+        ref = dev(_r((B, T, C), 139))
+        K.opconv(pl2, C, w2, b2, 1, prec, residual=x, out_scale=1 / 3, accumulate_into=ref, dense=True)
+    if grid:
+        monkeypatch.setenv("ALCM_AMPAIR_GRID", str(grid))
+        _hip.reload_knobs()
+    try:
+        if mode == "state":
+            y = K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec)
+        else:
+            y = dev(_r((B, T, C), 139))
+            K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec, out_scale=1 / 3, accumulate_into=y, last=True)
+    finally:
+        if grid:
+            monkeypatch.delenv("ALCM_AMPAIR_GRID")
+            _hip.reload_knobs()
+    y, ref = y.cpu(), ref.cpu()
+    assert torch.isfinite(y).all()
+    d = (y - ref).abs().max().item()
+    print(f"ampair C{C} T{T} k{k} d{dil} {mode}: max |diff| {d:.3e} equal {torch.equal(y, ref)}")
+    assert rel_l2(y.numpy(), ref.numpy()) < 2e-6

@@ -47,6 +47,29 @@ def test_text_encode_mixed_policy(enc):
     assert err < 3e-3
 
 
+@pytest.mark.parametrize("policy,tol", [(True, 1e-4), ("mixed", 3e-3)])
+def test_text_encode_batch32_matches_reference(enc, policy, tol):
+    """The benchmarked batch (bench.py components.text_encode: 32 prompts x 77 tokens per tower, M = 2464 rows per
+    linear) takes other kernel choices than B = 2 (M = 154): the 96-column under-filled opconv tiles, the plane path at
+    full occupancy.  The golden's two prompts tiled to B = 32 (alternating order): every row must match its reference
+    row within the policy's tolerance, so those choices are pinned end to end (modules.py:567-582)."""
+    g = golden("text_B2_L77.npz")
+    sel = torch.arange(32) % 2
+    sel[16:] = 1 - sel[16:]
+    a = torch.from_numpy(g["clap_ids"])[sel]
+    b = torch.from_numpy(g["t5_ids"])[sel]
+    enc.set_split(policy)
+    try:
+        out = enc.encode_ids(a, b).cpu().numpy()
+    finally:
+        enc.set_split(True)
+    assert out.shape == (32, 154, 1024) and np.isfinite(out).all()
+    ref = g["out"][sel.numpy()]
+    errs = [rel_l2(out[i], ref[i]) for i in range(32)]
+    print(f"text B=32 {policy}: max row rel-L2 {max(errs):.2e}, whole {rel_l2(out, ref):.2e}")
+    assert max(errs) < tol
+
+
 def test_text_encode_mixed_t5_ffn_beyond_fp16_range():
     """T5 v1.1 FFN activations exceed 65504 on real weights (transformers keeps DenseReluDense.wo in fp32).  Scale
     the recipe's wi_0 / wi_1 by 150 (and wo by 1/150^2) so block 0's wo input peaks far above the fp16 range: the
