@@ -53,7 +53,7 @@ def parse_args(argv: Optional[Sequence[str]] = None):
     p.add_argument("--synthetic-tokenizer", action="store_true",
                    help="with -r: use the hash-id tokenizer stand-in when the tokenizer directories are absent")
     p.add_argument("--batch-size", type=int, default=32, help="prompts per batched generation")
-    p.add_argument("--seed", type=int, default=0, help="per-prompt RNG seeds are seed + prompt index")
+    p.add_argument("--seed", type=int, default=0, help="per-clip RNG seeds: seed + (prompt * n_iter + iteration) * n_samples + sample")
     p.add_argument("--precision", choices=["split", "mixed", "bf16"], default="mixed",
                    help="MFMA precision policy (DESIGN.md §3)")
     p.add_argument("--test-dataset-tsv", type=str, default=None, help="override the config's test_dataset tsv_path")

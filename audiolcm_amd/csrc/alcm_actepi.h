@@ -90,6 +90,47 @@ __device__ __forceinline__ void act_run_interior(const f32x2 (&win)[R + 12], con
   }
 }
 
+// Activation1d of R consecutive outputs j0 .. j0+R-1 near a sequence end, from a register window of CLAMPED input
+// rows win[i] = x[clamp(j0 - 6 + i, 0, T - 1)] (UpSample1d's replicate padding of x): every upsampled sample m of the
+// run is computed once (index math compile-time, as act_run_interior), then DownSample1d's replicate padding of the
+// upsampled signal (m outside [0, 2T) takes the value at 0 / 2T - 1, both inside the run when needed) by selects, then
+// the down filter.  The same sums in the same order as act_one_clamped: bit-identical to it, with the window loads
+// issued together instead of one dependent load per tap (outputs j outside [0, T) are the caller's to mask)
+template <int R>
+__device__ __forceinline__ void act_run_edge(const f32x2 (&win)[R + 12], int j0, int T, const Taps12O& f, f32x2 ear,
+                                             f32x2 h, f32x2 (&o)[R]) {
+  constexpr int NQ = 2 * R + 10;
+  f32x2 sv[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    f32x2 u = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int k = 2 * kk + (q & 1);
+      u = fma2(f32x2{f.up[k], f.up[k]}, win[(q - k) / 2 + 6], u);
+    }
+    sv[q] = snake2(u, ear, h);
+  }
+  const int m0 = 2 * j0 - 5;
+  f32x2 slo = sv[0], shi = sv[NQ - 1];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (m0 + q == 0) slo = sv[q];
+    if (m0 + q == 2 * T - 1) shi = sv[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (m0 + q < 0) sv[q] = slo;
+    if (m0 + q >= 2 * T) sv[q] = shi;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    o[r] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sv[2 * r + k], o[r]);
+  }
+}
+
 // One output j anywhere in [0, T): replicate padding of the up filter's input (pad 5) and of the down
 // filter's input (pad 5 / 6) as index clamps.  ld(i) returns input row i (0 <= i < T) of the pair.
 template <typename LD>

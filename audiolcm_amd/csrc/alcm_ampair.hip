@@ -96,12 +96,16 @@ __device__ __forceinline__ void ap_wait_barrier() {
 }
 
 // Activation1d rows [0, n) of one tile: output row lr is global row t_org + lr, written as fp16 into the operand rows
-// dst + lr * RS (rows outside [0, T): zeros); ld(i) returns input row i (global index, 0 <= i < T) of pair p.
-// Work item = (run of R rows, channel pair), pairs fastest.
+// dst + lr * RS (rows outside [0, T): zeros); ld(i, p) returns input row i of pair p for ANY 0 <= i < T (the caller's
+// loader also clamps to its own storage).  Work item = (run of R rows, channel pair), pairs fastest.  A run whose
+// window lies inside [0, T) takes act_run_interior (a partial last run computes R rows and stores jn); runs at the
+// sequence ends take act_run_edge on clamped windows, R/2 rows at a time (register budget)
 template <int R, int NP, int RS, int NT, class LD>
 __device__ __forceinline__ void ap_act(int n, int t_org, int T, const Taps12O& f, const float* ae, const float* ib,
                                        int c0, char* dst, int tid, LD ld) {
   constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int RH = R / 2;
+  static_assert(R % 2 == 0, "edge halves");
   const int nrun = (n + R - 1) / R;
   for (int w = tid; w < NP * nrun; w += NT) {
     const int run = w / NP, p = w - run * NP;
@@ -111,20 +115,30 @@ __device__ __forceinline__ void ap_act(int n, int t_org, int T, const Taps12O& f
     const f32x2 ear = f32x2{ae[c], ae[c + 1]} * INV_PI;
     const f32x2 h = f32x2{ib[c], ib[c + 1]} * 0.5f;
     char* d = dst + lr0 * RS + c * 2;
-    if (jn == R && t0 >= 6 && t0 + R + 6 <= T) {
+    if (t0 >= 6 && t0 + jn + 6 <= T) {
       f32x2 win[R + 12];
 #pragma unroll
-      for (int i = 0; i < R + 12; ++i) win[i] = ld(t0 - 6 + i, p);
+      for (int i = 0; i < R + 12; ++i) win[i] = ld(min(t0 - 6 + i, T - 1), p);
       f32x2 o[R];
       act_run_interior<R>(win, f, ear, h, o);
 #pragma unroll
-      for (int r = 0; r < R; ++r) ap_st2(d + r * RS, o[r]);
+      for (int r = 0; r < R; ++r)
+        if (r < jn) ap_st2(d + r * RS, o[r]);
     } else {
-      for (int r = 0; r < jn; ++r) {
-        const int t = t0 + r;
-        f32x2 o = f32x2{0.f, 0.f};
-        if (t >= 0 && t < T) o = act_one_clamped(t, T, f, ear, h, [&](int i) { return ld(i, p); });
-        ap_st2(d + r * RS, o);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        if (hh * RH >= jn) break;
+        const int j0 = t0 + hh * RH;
+        f32x2 win[RH + 12];
+#pragma unroll
+        for (int i = 0; i < RH + 12; ++i) win[i] = ld(min(max(j0 - 6 + i, 0), T - 1), p);
+        f32x2 o[RH];
+        act_run_edge<RH>(win, j0, T, f, ear, h, o);
+#pragma unroll
+        for (int r = 0; r < RH; ++r) {
+          const int t = j0 + r;
+          if (hh * RH + r < jn) ap_st2(d + (hh * RH + r) * RS, (t >= 0 && t < T) ? o[r] : f32x2{0.f, 0.f});
+        }
       }
     }
   }
@@ -235,23 +249,7 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
     // ---- 2. conv1
     kloop(abuf, P.dil, gs0);
 
-    // residual rows of this wave's conv2 outputs (row e0 + wave TM 16 + 16 i + 4 q4 + r, column 16 j + l16), loaded
-    // under act2
     float rv[TM][TN][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int r2 = wave * TM * 16 + i * 16 + q4 * 4 + r;
-        const int t = e0 + r2;
-        const bool okr = r2 < E && t < T;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = j * 16 + l16;
-          rv[i][j][r] = (okr && n < C) ? xb[(int64_t)t * C + n] : 0.f;
-        }
-      }
-
     // ---- 3. act2 per channel group: conv1 + bias -> LDS, then Activation1d -> a2 rows [s1 + 6, s1 + CR - 6)
 #pragma unroll
     for (int g = 0; g < G::NG; ++g) {
@@ -268,9 +266,26 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
           }
         }
       __syncthreads();
+      if (g == G::NG - 1) {
+        // residual rows of this wave's conv2 outputs (row e0 + wave TM 16 + 16 i + 4 q4 + r, column 16 j + l16),
+        // loaded under the last group's act2 (the accumulators are dead by then: no register overlap)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int r2 = wave * TM * 16 + i * 16 + q4 * 4 + r;
+            const int t = e0 + r2;
+            const bool okr = r2 < E && t < T;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int n = j * 16 + l16;
+              rv[i][j][r] = (okr && n < C) ? xb[(int64_t)t * C + n] : 0.f;
+            }
+          }
+      }
       ap_act<R, V1C / 2, RS, NT>(CR - 12, s1 + 6, T, P.f2, P.ae2, P.ib2, g * V1C, abuf, tid,
-                                  [&](int i, int p) {
-                                    return *reinterpret_cast<const f32x2*>(v1 + (i - s1) * V1S + 2 * p);
+                                  [&](int i, int p) {  // (rows past the staged tile: a partial run's unused tail)
+                                    return *reinterpret_cast<const f32x2*>(v1 + min(i - s1, CR - 1) * V1S + 2 * p);
                                   });
       __syncthreads();
     }

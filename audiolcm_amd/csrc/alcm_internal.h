@@ -89,12 +89,12 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
-  int wconv = 8;                 // ALCM_WCONV: 8 = 2-workgroup/CU kernel, 5 = 256-row kernel, 0 = neither
+  int wconv = 8;                 // ALCM_WCONV: > 0 = the wide-layer kernels (alcm_wconv.hip), 0 = opconv_kernel (A/B)
   int wconv_order = -1;          // ALCM_WCONV_ORDER: wconv2 workgroup order (-1 by shape, 0 M-tile major, 1 N-tile major)
   int wconv_ablate = 0;          // ALCM_WCONV_ABLATE: timing-only ablation bits of the wide-layer kernel
   int wconv_fpipe = 1;           // ALCM_WCONV_FPIPE: wconv2 fragment-pipelined K loop (0 = per-slice read-then-MFMA)
   int wconv3 = -1;               // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip): -1 by shape, 0 off, 1 on
-  int w3_epi = 1;                // ALCM_W3_EPI: wconv3 fp32 epilogue with 16-B accesses after an in-quad transpose (0: 4-B column accesses)
+  int w3_epi = 0;                // ALCM_W3_EPI: 1 = opt-in wconv3 fp32 epilogue with 16-B accesses after an in-quad transpose (default 0: 4-B column accesses, -0.7 % end to end with 1)
   bool text_gemm = false;        // ALCM_TEXT_GEMM: text encoders' F16 / BF16 linears on the fp32-A GEMM (A/B; default: planes)
   int wconv3_grid = 0;           // ALCM_WCONV3_GRID: cap on wconv3's persistent workgroups (tests; 0 = one per CU)
   int wconv_tile = -1;           // ALCM_WCONV_TILE: wconv2 tile, 0 = 128 x 192, 1 = 256 x 96, -1 = by shape

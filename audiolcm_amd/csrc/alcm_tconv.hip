@@ -479,6 +479,7 @@ static int tc2_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, 
 int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const ActEpiDev* act, double flops,
           double bytes, hipStream_t s) {
   if (!tconv_supported(a.prec, a.C, a.N, a.ksize, a.dil)) return set_error(ALCM_E_INVALID, "tconv: unsupported shape");
+  if (a.C <= 0 || a.Cp < a.C || a.ksize < 1 || a.dil < 1) return set_error(ALCM_E_INVALID, "tconv: bad geometry");
   if (kd != (a.ksize * a.C + 31) / 32 * 32 || !wd) return set_error(ALCM_E_INVALID, "tconv: dense weight layout");
   if (2 * a.pad != (a.ksize - 1) * a.dil || a.out_stride > 0 || a.out_act || a.geglu_plane)
     return set_error(ALCM_E_INVALID, "tconv: same-length convs only");

@@ -1,21 +1,12 @@
-// Wide implicit-GEMM conv1d for the MFMA-bound BigVGAN AMPBlock layers (C = N in {768, 384, 192};
-// vocoder/bigvgan/models.py:72-81), on the operand planes act_op_kernel writes (alcm_opconv.hip).
-//
-// Structure (gfx950, one 512-thread workgroup per CU):
-//   * output tile 256 rows (b, t) x BN columns, 8 waves as 2 (M) x 4 (N), each wave 128 x BN/4 built from
-//     16x16x32 MFMAs with fp32 accumulators;
-//   * K runs over (64-channel chunk, tap) steps.  The input window of a chunk, rows
-//     [t0 - pad, t0 + 256 + (k-1)d - pad) x 64 channels (<= 320 rows x 128 B), is staged once per chunk
-//     and read by every tap at row offset tap*d; the weight tile of a step (BN rows x 128 B) is staged
-//     per step;
-//   * staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip): windows double-buffered across
-//     chunks, weight tiles triple-buffered so two steps are in flight, with counted `s_waitcnt vmcnt`
-//     and raw barriers (a __syncthreads would drain the DMA queue every step);
-//   * LDS images are lane-linear (one DMA instruction = 8 rows of 128 B); the 16-B slot of logical slot
-//     s in row r is s ^ (r & 7), applied on the DMA source address and on the fragment read, which makes
-//     the ds_read_b128 fragment reads conflict-free at ANY start row (the tap offset tap*d is arbitrary);
-//   * rows outside [0, T) read a zero line (per-lane source address select, no masking pass);
-//   * XCD-aware tile order: the N tiles of one M tile (which share the input window) run on one XCD.
+// Wide implicit-GEMM conv1d on MFMA operand planes (fp16 / bf16) for the MFMA-bound layers: BigVGAN stage 0-2
+// AMPBlock convs and upsampler phases (vocoder/bigvgan/models.py:72-81, 160-165), the DiT FFN / attention projections
+// (ldm/modules/new_attention.py:48-74), the VAE k3 convs and the text encoders' wide linears.  Two kernels:
+//   * wconv2_kernel: 4 waves, two workgroups per CU (128 x 192 or 256 x 96 tiles), window staged per 64-channel
+//     chunk, weights double-buffered; strided (ConvTranspose phase), GEGLU-plane and fused-Activation1d epilogues;
+//   * wconv3_kernel: one persistent 8-wave workgroup per CU walking a flat (tile, chunk, tap) step sequence.
+// Common: LDS-DMA staging (global_load_lds_dwordx4, no VGPR round trip) into lane-linear images whose 16-B slot s of
+// row r sits at s ^ (r & 7) (conflict-free ds_read_b128 fragment reads from any start row); rows outside [0, T) read
+// a zero line; XCD-aware workgroup order.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -53,312 +44,9 @@ struct WConvDev {
                         // 2 no MFMA, 4 no global -> LDS staging in the K loop
 };
 
-constexpr int WC_BM = 256;
-constexpr int WC_WROWS = 320;  // staged window rows: 256 + (k-1)*d <= 320
-constexpr int WC_WPW = WC_WROWS / 8 / 8;  // window DMA instructions per wave (5)
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
-}
-
-template <int BN, int PREC, int VAR, bool ACT>
-__global__ __launch_bounds__(512) void wconv_kernel(const WConvDev P) {
-  constexpr int TN = BN / 64;            // 16-col fragments per wave (wave covers BN/4 columns)
-  constexpr int BPW = BN / 64;           // weight DMA instructions per wave per step (BN/8 rows-of-8 / 8 waves)
-  constexpr int WBUF = WC_WROWS * 128;   // bytes of one window image
-  constexpr int BBUF = BN * 128;         // bytes of one weight image
-  constexpr int SMEM = 2 * WBUF + 3 * BBUF;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-
-  // XCD-aware tile order (bijective for any nwg): consecutive work ids run on one XCD
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q = P.nwg >> 3, r8 = P.nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
-  const int mt = wid / P.tiles_n, nt = wid - mt * P.tiles_n;
-  const int b = mt / P.tiles_per_batch;
-  const int t0 = (mt - b * P.tiles_per_batch) * P.tstride - P.tshift;
-  const int col0 = nt * BN;
-  const int K = P.ksize, Cp = P.Cp;
-  const int WR = WC_BM + (K - 1) * P.dil;
-  const int nC = Cp / 64;
-  const int steps = nC * K;
-
-  // window DMA sources: instruction i = wave + 8j covers rows 8i .. 8i+7; lane -> (row, physical slot)
-  const u16* wsrc[WC_WPW];
-  int wstep[WC_WPW];
-#pragma unroll
-  for (int j = 0; j < WC_WPW; ++j) {
-    const int row = 8 * (wave + 8 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (row & 7);
-    const int ts = t0 - P.pad + row;
-    const bool ok = row < WR && ts >= 0 && ts < P.T;
-    wsrc[j] = ok ? P.a + ((int64_t)b * P.T + ts) * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
-    wstep[j] = ok ? 64 : 0;
-  }
-  // weight DMA sources
-  const u16* bsrc[BPW];
-#pragma unroll
-  for (int j = 0; j < BPW; ++j) {
-    const int n = 8 * (wave + 8 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (n & 7);
-    bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
-  }
-  const bool no_dma = (P.ablate & 4) != 0, no_mfma = (P.ablate & 2) != 0;
-  auto stage_w = [&](int c, int buf) {
-    if (no_dma && c > 0) return;
-#pragma unroll
-    for (int j = 0; j < WC_WPW; ++j) glds16(wsrc[j] + c * wstep[j], smem + buf * WBUF + (wave + 8 * j) * 1024);
-  };
-  auto stage_b = [&](int s, int buf) {
-    if (no_dma && s > 1) return;
-    const int c = s / K, tap = s - c * K;
-    const int off = tap * Cp + c * 64;
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) glds16(bsrc[j] + off, smem + 2 * WBUF + buf * BBUF + (wave + 8 * j) * 1024);
-  };
-
-  f32x4 acc[8][TN];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment read geometry: lane reads row (l & 15) of each 16-row block, logical slot 4*sub + (l >> 4)
-  const int arow0 = wm * 128 + (lane & 15);
-  const int nrow0 = wn * (BN / 4) + (lane & 15);
-  const int bsw = lane & 7;  // (n & 7) of every B fragment row of this lane
-
-  // prologue: window 0 + weight steps 0 and 1 in flight; wait for all but the last step's 3
-  stage_w(0, 0);
-  stage_b(0, 0);
-  stage_b(steps > 1 ? 1 : 0, 1);
-  if constexpr (BPW == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  asm volatile("s_barrier" ::: "memory");
-
-  int s = 0;
-  for (int c = 0; c < nC; ++c) {
-    const int wb = c & 1;
-    for (int tap = 0; tap < K; ++tap, ++s) {
-      const bool wnext = tap == 0 && c + 1 < nC;
-      if (wnext) stage_w(c + 1, wb ^ 1);
-      stage_b(s + 2 < steps ? s + 2 : steps - 1, (s + 2) % 3);
-
-      const char* Wl = smem + wb * WBUF;
-      const char* Bl = smem + 2 * WBUF + (s % 3) * BBUF;
-      const int arow = arow0 + tap * P.dil;
-      const int asw = arow & 7;
-      if constexpr ((VAR & 3) == 0) {
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const int ls = 4 * sub + (lane >> 4);
-          bf16x8 af[8], bfr[TN];
-          const char* ap = Wl + arow * 128 + ((ls ^ asw) << 4);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
-          const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
-          if (no_mfma) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
-#pragma unroll
-            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bfr[j]));
-            continue;
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
-        }
-      } else {
-        // all fragments of the step first (22 x ds_read_b128), then the 48 MFMAs at raised priority
-        bf16x8 af[2][8], bfr[2][TN];
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const int ls = 4 * sub + (lane >> 4);
-          const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[sub][j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
-          const char* ap = Wl + arow * 128 + ((ls ^ asw) << 4);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) af[sub][i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
-        }
-        if constexpr ((VAR & 3) == 2) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[sub][i], bfr[sub][j], acc[i][j]);
-        if constexpr ((VAR & 3) == 2) __builtin_amdgcn_s_setprio(0);
-      }
-      // weight step s+1 (issued one step earlier) must have landed before the barrier; everything
-      // issued after it (this step's window and weight DMA) stays in flight across the barrier
-      if (wnext) {
-        if constexpr (BPW == 3) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      } else {
-        if constexpr (BPW == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (P.ablate & 1) {
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    asm volatile("" ::"v"(sum));
-    return;
-  }
-
-  if constexpr (ACT) {
-    // v = conv + bias (+ res) -> LDS, one half of the tile's columns at a time (all 256 rows: the
-    // activation needs the halo rows); fp32 out (if any) for the owned rows; Activation1d -> planes
-    constexpr int HC = BN / 2;      // columns per half
-    constexpr int OTS = HC + 4;
-    float* ot = reinterpret_cast<float*>(smem);
-    const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
-    for (int h = 0; h < 2; ++h) {
-      if ((wn >> 1) == h) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              const int nl = (wn & 1) * (BN / 4) + j * 16 + (lane & 15);
-              ot[(wm * 128 + i * 16 + (lane >> 4) * 4 + r) * OTS + nl] =
-                  acc[i][j][r] + (P.bias ? P.bias[col0 + h * HC + nl] : 0.f);
-            }
-      }
-      __syncthreads();
-      if (P.res || P.out) {
-        constexpr int cq = HC / 4;
-        for (int e = tid; e < WC_BM * cq; e += 512) {
-          const int m = e / cq, n = (e - m * cq) * 4;
-          const int t = t0 + m;
-          if (t < 0 || t >= P.T) continue;
-          const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + h * HC + n;
-          float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-          if (P.res) {
-            const float4 rv = *reinterpret_cast<const float4*>(P.res + go);
-            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-            *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
-          }
-          if (P.out && t >= e_lo && t < e_hi) {
-            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
-            if (P.accumulate) {
-              const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
-              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
-            }
-            *reinterpret_cast<float4*>(P.out + go) = v;
-          }
-        }
-        __syncthreads();
-      }
-      act_epilogue_tile<PREC, 15>(ot, OTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 512);
-      __syncthreads();
-    }
-    return;
-  }
-  if constexpr ((VAR & 4) != 0) {
-    // LDS-staged epilogue: one 128-row half of the tile at a time goes through LDS (the K loop's last
-    // barrier retired every fragment read) and leaves as whole row segments with 16-B residual loads
-    // and stores
-    constexpr int OTS = BN + 4;  // floats per staged row
-    float* ot = reinterpret_cast<float*>(smem);
-    const int cq = BN / 4;       // float4 per row segment
-    for (int h = 0; h < 2; ++h) {
-      if (wm == h) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              ot[(i * 16 + (lane >> 4) * 4 + r) * OTS + wn * (BN / 4) + j * 16 + (lane & 15)] = acc[i][j][r];
-      }
-      __syncthreads();
-      const int r0 = t0 + h * 128;
-      constexpr int PER = 128 * (BN / 4) / 512;
-      if (P.gplane) {
-        // GEGLU (new_attention.py:48-55): columns (2j, 2j+1) = (value j, gate j) -> v * gelu_erf(gate)
-        const int No = P.N / 2;
-        for (int e = 0; e < PER; ++e) {
-          const int idx = tid + e * 512;
-          const int m = idx / cq, n = (idx - m * cq) * 4;
-          if (r0 + m >= P.T) continue;
-          float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-          if (P.bias) {
-            const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
-            v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-          }
-          f32x2 y;
-          y.x = v.x * alcm_act(v.y, ACT_GELU_ERF);
-          y.y = v.z * alcm_act(v.w, ACT_GELU_ERF);
-          op_store2<PREC>(P.gplane + ((int64_t)b * P.T + r0 + m) * No + (col0 + n) / 2, 0, y);
-        }
-        __syncthreads();
-        continue;
-      }
-      float4 rv[PER], pv[PER];
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int idx = tid + e * 512;
-        const int m = idx / cq, n = (idx - m * cq) * 4;
-        const int t = min(r0 + m, P.T - 1);
-        const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + col0 + n;
-        rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
-        pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int e = 0; e < PER; ++e) {
-        const int idx = tid + e * 512;
-        const int m = idx / cq, n = (idx - m * cq) * 4;
-        if (r0 + m >= P.T) continue;
-        const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
-        float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        if (P.bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
-          v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-        }
-        v.x = (v.x + rv[e].x) * P.out_scale + pv[e].x;
-        v.y = (v.y + rv[e].y) * P.out_scale + pv[e].y;
-        v.z = (v.z + rv[e].z) * P.out_scale + pv[e].z;
-        v.w = (v.w + rv[e].w) * P.out_scale + pv[e].w;
-        *reinterpret_cast<float4*>(P.out + go) = v;
-      }
-      __syncthreads();
-    }
-    return;
-  }
-  // epilogue: direct stores from the accumulators (16 lanes x 4 B contiguous per row)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = t0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-      if (t >= P.T) continue;
-      const int64_t ro = ((int64_t)b * P.T + t) * P.N;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = col0 + wn * (BN / 4) + j * 16 + (lane & 15);
-        float v = acc[i][j][r];
-        if (P.bias) v += P.bias[n];
-        if (P.res) v += P.res[ro + n];
-        v *= P.out_scale;
-        if (P.accumulate) v += P.out[ro + n];
-        P.out[ro + n] = v;
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1174,27 +862,29 @@ static bool wconv2_tile256(const alcm_opconv_args& a) {
   return a.out_stride <= 0 && a.ksize >= 7 && mt * (a.N / 96) >= 256;
 }
 
-// Eligible: single-plane precisions, N a multiple of 128, Cp a multiple of 64, 2 <= k, (k-1)d <= 64,
-// no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel.
+// Eligible: single-plane precisions, N a multiple of 192 (128 x 192 tiles) or 96 (256 x 96 tiles), Cp a multiple of
+// 64, (k-1)d <= 64, no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel
+// (ALCM_WCONV=0: always 0 for plain same-length convs, the A/B reference; strided / GEGLU / fused-activation
+// epilogues exist only here).
 int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s) {
-  const int var = knobs().wconv;
+  const bool off = knobs().wconv <= 0;
+  const bool strided = a.out_stride > 0;
+  const bool act = actepi != nullptr;
   // persistent 8-wave kernel (ALCM_WCONV3: -1 by shape, 0 off, 1 wherever eligible): by shape where the 256-row
   // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %),
   // not for the GEGLU up-projection (its register epilogue evaluates erf on every lane: 5.25 vs 4.94 ms/step)
   const int w3 = knobs().wconv3;
   const int mt256 = (a.T + W3_BM - 1) / W3_BM;
-  if (w3 != 0 && !actepi && a.out_stride <= 0 &&
+  if (!off && w3 != 0 && !act && !strided &&
       (w3 > 0 || (a.T * 100 >= mt256 * W3_BM * 85 && !a.geglu_plane)) && wconv3_try(a, wplane, flops, bytes, s))
     return 1;
-  const bool strided = a.out_stride > 0;  // diagnostics / A-B: 0 = opconv_kernel, 7 = setprio K loop      // default: plain K loop + LDS-staged epilogue (measured best)
-  const bool act = actepi != nullptr;
-  if (var <= 0 && !act && !a.geglu_plane && !strided) return 0;
+  if (off && !act && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > WC_WROWS - WC_BM) return 0;
-  const int BN = a.N % 192 == 0 ? 192 : (a.N % 128 == 0 ? 128 : 0);
-  if (!BN) return 0;
-  if (!act && !a.geglu_plane && !strided && (int64_t)a.B * a.T < 4 * WC_BM) return 0;  // small problems: the 128-row kernel fills the chip better
+  if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > W2_HALO) return 0;
+  if (a.N % 96) return 0;
+  if (!act && !a.geglu_plane && !strided && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
+                                                                                     // 128-row tiles fill the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
@@ -1202,7 +892,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   const int tk = knobs().wconv_tile;
   const bool t256 = !act && a.N % 96 == 0 && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
   const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
-  if ((var == 8 || strided) && !(act && strided) && a.N % BN2 == 0 && (a.ksize - 1) * a.dil <= W2_HALO) {
+  if (!(act && strided) && a.N % BN2 == 0) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
@@ -1271,51 +961,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     }
     return 1;
   }
-  if (strided) return 0;
-  WConvDev P{};
-  P.a = (const u16*)a.a;
-  P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
-  P.ostride = 1; P.ooff = 0; P.orows = a.T;
-  P.w = wplane; P.kpad = a.kpad; P.N = a.N;
-  P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
-  P.gplane = (u16*)a.geglu_plane;
-  P.ablate = knobs().wconv_ablate;
-  // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 256 conv rows and emits 256 - 2 * HALO
-  P.tstride = act ? WC_BM - 2 * ACT_EPI_HALO : WC_BM;
-  P.tshift = act ? ACT_EPI_HALO : 0;
-  if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
-  P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
-  P.tiles_n = a.N / BN;
-  const int64_t nwg = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
-  if (nwg >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
-  P.nwg = (int)nwg;
-  void* tok = prof_start(s);
-  const dim3 grid((unsigned)nwg), blk(512);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, blk, 0, s, P); };
-  auto pick = [&](auto vc, auto ac) {
-    constexpr int V = decltype(vc)::value;
-    constexpr bool A = decltype(ac)::value;
-    if (BN == 192) {
-      if (a.prec == PREC_F16) go(wconv_kernel<192, PREC_F16, V, A>);
-      else go(wconv_kernel<192, PREC_BF16, V, A>);
-    } else {
-      if (a.prec == PREC_F16) go(wconv_kernel<128, PREC_F16, V, A>);
-      else go(wconv_kernel<128, PREC_BF16, V, A>);
-    }
-  };
-  const int V = (!act && !a.geglu_plane && var == 7) ? 6 : 4;
-  if (act) pick(std::integral_constant<int, 4>{}, std::true_type{});
-  else if (V == 6) pick(std::integral_constant<int, 6>{}, std::false_type{});
-  else pick(std::integral_constant<int, 4>{}, std::false_type{});
-  if (tok) {
-    char name[80];  // the demangled rocprofv3 name of the instantiation
-    std::snprintf(name, sizeof(name), "alcm::wconv_kernel<%d, %d, %d, %s>", BN, a.prec, V, act ? "true" : "false");
-    if (knobs().prof_shapes)  // diagnostics: split the statistics per layer shape
-      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
-                    a.ksize);
-    prof_stop(tok, s, name, flops, bytes);
-  }
-  return 1;
+  return 0;  // opconv_kernel
 }
 
 }  // namespace alcm

@@ -396,7 +396,8 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
         fd = fd.detach().reshape(-1).float().cpu().contiguous()
         cpo = _round_up(N, 32)
         nplo = 2 if prec == _hip.PREC_SPLIT else 1
-        y = torch.empty((nplo, B, T, cpo), dtype=torch.int16, device=planes.device)
+        # (dense=True writes channels < N only: zero planes keep the operand padding safe for any consumer)
+        y = (torch.zeros if dense else torch.empty)((nplo, B, T, cpo), dtype=torch.int16, device=planes.device)
         keep = [ae, ib, fu, fd]
         a.act_plane, a.act_plane_lo_off = ptr(y), B * T * cpo
         a.act_alpha_exp, a.act_inv_beta = ptr(ae), ptr(ib)

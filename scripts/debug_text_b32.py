@@ -15,8 +15,8 @@ enc = CLAPT5TextEncoder.from_recipe(0, split="mixed")
 for B in (2, 4, 8, 16, 32):
     sel = torch.arange(B) % 2
     a, b = torch.from_numpy(g["clap_ids"])[sel], torch.from_numpy(g["t5_ids"])[sel]
-    for knob in ("", "ALCM_OPCONV_TILE=-1", "ALCM_TEXT_GEMM=1"):
-        for k in ("ALCM_OPCONV_TILE", "ALCM_TEXT_GEMM"):
+    for knob in ("", "ALCM_WCONV=0", "ALCM_TEXT_GEMM=1"):
+        for k in ("ALCM_WCONV", "ALCM_TEXT_GEMM"):
             os.environ.pop(k, None)
         if knob:
             k, v = knob.split("=")

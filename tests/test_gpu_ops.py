@@ -344,18 +344,19 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
     y = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5, accumulate_into=acc).cpu() - 1
     assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
     from audiolcm_amd import _hip
-    # the default (2-workgroup/CU, 128 x 192 tiles) vs the 256-row kernel (ALCM_WCONV=5) and opconv_kernel (0)
-    for var in ("5", "0"):
-        monkeypatch.setenv("ALCM_WCONV", var)
+    # the default (wconv3 where its tiles are full, else the two-workgroup kernel) vs each wide kernel forced
+    # (ALCM_WCONV3=1 / 0) and vs opconv_kernel (ALCM_WCONV=0: no wide kernel at all)
+    for knob, var in (("ALCM_WCONV3", "1"), ("ALCM_WCONV3", "0"), ("ALCM_WCONV", "0")):
+        monkeypatch.setenv(knob, var)
         _hip.reload_knobs()
         try:
             acc0 = dev(torch.ones((B, T, C)))
             y0 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
                           accumulate_into=acc0).cpu() - 1
         finally:
-            monkeypatch.delenv("ALCM_WCONV")
+            monkeypatch.delenv(knob)
             _hip.reload_knobs()
-        assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
+        assert rel_l2(y.numpy(), y0.numpy()) < 1e-5, (knob, var)
 
 
 @pytest.mark.parametrize("C,T,k,dil,grid", [(384, 1100, 7, 3, 0), (384, 1100, 7, 3, 8), (192, 1500, 3, 1, 16),
