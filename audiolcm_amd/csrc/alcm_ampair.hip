@@ -49,11 +49,13 @@ struct APairDev {
   const float* ib2;
   Taps12O f1, f2;
   int tiles_per_batch, ntiles;
+  int ablate;  // diagnostics (ALCM_AMPAIR_ABLATE, timing only, results wrong): 1 no act1, 2 no act2, 4 no MFMAs,
+               // 8 no output stores
 };
 
-template <int C, int NPB, int KS, int CR>
+template <int C, int NPB, int KS, int CR, int NW_, int V1C_>
 struct APairGeo {
-  static constexpr int NW = 8, NT = NW * 64;
+  static constexpr int NW = NW_, NT = NW * 64;
   static constexpr int TM = CR / 16 / NW;                 // 16-row M tiles per wave
   static constexpr int NSP = (C + 15) / 16 * 16, TN = NSP / 16;
   static constexpr int P2 = (KS - 1) / 2;
@@ -63,7 +65,7 @@ struct APairGeo {
   static constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;  // operand row: odd number of 16-B slots
   static constexpr int RS = RSS * 16;
   static constexpr int A1B = (A1R * RS + 1023) / 1024 * 1024;
-  static constexpr int V1C = C < 48 ? C : 48, NG = C / V1C;  // conv1 output staged in groups of <= 48 channels
+  static constexpr int V1C = V1C_, NG = C / V1C;          // conv1 output staged in groups of V1C channels
   static constexpr int V1S = V1C + 2;                     // staged row stride (floats)
   static constexpr int V1B = (CR * V1S * 4 + 1023) / 1024 * 1024;
   static constexpr int KD = (KS * C + 31) / 32 * 32;      // dense K
@@ -75,7 +77,7 @@ struct APairGeo {
   static constexpr int SMEM = A1B + V1B + RING * SLOT + 1024;
   static_assert(C % 16 == 8 || C % 16 == 0, "C % 8");
   static_assert(CR % (16 * NW) == 0 && SLOT % 1024 == 0 && C % V1C == 0 && V1C % 2 == 0, "geometry");
-  static_assert(SMEM <= 163840, "LDS");
+  static_assert(SMEM <= (NW == 4 ? 81920 : 163840), "LDS (4 waves: two workgroups per CU)");
 };
 
 __device__ __forceinline__ void ap_glds16(const void* src, char* lds) {
@@ -144,9 +146,9 @@ __device__ __forceinline__ void ap_act(int n, int t_org, int T, const Taps12O& f
   }
 }
 
-template <int C, int NPB, int KS, int CR, int R, bool LAST>
-__global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
-  using G = APairGeo<C, NPB, KS, CR>;
+template <int C, int NPB, int KS, int CR, int NW, int V1C_, int R, bool LAST>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const APairDev P) {
+  using G = APairGeo<C, NPB, KS, CR, NW, V1C_>;
   constexpr int NT = G::NT, TM = G::TM, TN = G::TN, NSP = G::NSP, RS = G::RS, NS = G::NS;
   constexpr int E = G::E, P2 = G::P2, V1C = G::V1C, V1S = G::V1S, SLOT = G::SLOT;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
@@ -218,13 +220,20 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dl) * RS + c * 2);
+      if (P.ablate & 4) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (NPB == 2) acc[i][j] = mfma16<PREC_F16>(af[i], bl[j], acc[i][j]);
-          acc[i][j] = mfma16<PREC_F16>(af[i], bh[j], acc[i][j]);
-        }
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (NPB == 2) acc[i][j] = mfma16<PREC_F16>(af[i], bl[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_F16>(af[i], bh[j], acc[i][j]);
+          }
+      }
       if (more) ap_wait_barrier<G::DPW>();
       else ap_wait_barrier<0>();
     }
@@ -239,6 +248,7 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
     const int gs0 = it * 2 * NS;
 
     // ---- 1. act1: x -> a1 rows [s1 - p1, s1 + CR + p1)
+    if (!(P.ablate & 1))
     ap_act<R, C / 2, RS, NT>(CR + 2 * P.p1, s1 - P.p1, T, P.f1, P.ae1, P.ib1, 0, abuf, tid,
                               [&](int i, int p) {
                                 return *reinterpret_cast<const f32x2*>(
@@ -283,6 +293,7 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
             }
           }
       }
+      if (!(P.ablate & 2))
       ap_act<R, V1C / 2, RS, NT>(CR - 12, s1 + 6, T, P.f2, P.ae2, P.ib2, g * V1C, abuf, tid,
                                   [&](int i, int p) {  // (rows past the staged tile: a partial run's unused tail)
                                     return *reinterpret_cast<const f32x2*>(v1 + min(i - s1, CR - 1) * V1S + 2 * p);
@@ -298,7 +309,7 @@ __global__ __launch_bounds__(512) void ampair_kernel(const APairDev P) {
       for (int r = 0; r < 4; ++r) {
         const int r2 = wave * TM * 16 + i * 16 + q4 * 4 + r;
         const int t = e0 + r2;
-        if (r2 >= E || t >= T) continue;
+        if (r2 >= E || t >= T || (P.ablate & 8)) continue;
         float* orow = P.out + ((int64_t)b * T + t) * C;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -327,9 +338,9 @@ bool ampair_supported(int prec, int C, int ksize, int dil) {
 
 static int g_ap_ncu = 0;
 
-template <int C, int NPB, int KS, int CR>
+template <int C, int NPB, int KS, int CR, int NW, int V1C>
 static int ap_launch(const APairDev& P, bool last, hipStream_t s) {
-  using G = APairGeo<C, NPB, KS, CR>;
+  using G = APairGeo<C, NPB, KS, CR, NW, V1C>;
   if (!g_ap_ncu) {
     int dev = 0, n = 0;
     g_ap_ncu = (hipGetDevice(&dev) == hipSuccess &&
@@ -338,23 +349,32 @@ static int ap_launch(const APairDev& P, bool last, hipStream_t s) {
                    : 256;
   }
   const int R8 = (P.ntiles + 7) / 8;
-  int grid = 8 * std::min(g_ap_ncu / 8, R8);
+  int grid = 8 * std::min(g_ap_ncu * (NW == 4 ? 2 : 1) / 8, R8);
   if (knobs().ampair_grid >= 8) grid = std::min(grid, knobs().ampair_grid / 8 * 8);  // tests: several tiles per WG
-  if (last) hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, 16, true>), dim3(grid), dim3(G::NT), 0, s, P);
-  else hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, 16, false>), dim3(grid), dim3(G::NT), 0, s, P);
+  if (last) hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, 16, true>), dim3(grid), dim3(G::NT), 0, s, P);
+  else hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, 16, false>), dim3(grid), dim3(G::NT), 0, s, P);
   return 0;
 }
 
-template <int C, int NPB, int CR>
+template <int C, int NPB, int CR, int NW, int V1C>
 static int ap_by_k(const APairDev& P, int ksize, bool last, hipStream_t s) {
   switch (ksize) {
-    case 3: return ap_launch<C, NPB, 3, CR>(P, last, s);
-    case 7: return ap_launch<C, NPB, 7, CR>(P, last, s);
-    default: return ap_launch<C, NPB, 11, CR>(P, last, s);
+    case 3: return ap_launch<C, NPB, 3, CR, NW, V1C>(P, last, s);
+    case 7: return ap_launch<C, NPB, 7, CR, NW, V1C>(P, last, s);
+    default: return ap_launch<C, NPB, 11, CR, NW, V1C>(P, last, s);
   }
 }
 
-static int ap_emitted(int C, int ksize) { return (C == 24 ? 512 : 256) - 12 - (ksize - 1); }
+// tile geometry by width (ALCM_AMPAIR_NW: 0 by shape, 4 / 8 forced where the LDS allows): C = 24 / 48 as two 4-wave
+// workgroups per CU (<= 80 KB of LDS each: one's Activation1d phases (VALU) overlap the other's convs (MFMA) and load
+// latency), 256 conv rows; C = 96 one 8-wave workgroup per CU (its operand rows alone take 64 KB)
+static int ap_waves(int C) {
+  const int nw = knobs().ampair_nw;
+  if (C == 96) return 8;
+  return nw == 8 ? 8 : 4;
+}
+static int ap_rows(int C, int nw) { return (C == 24 && nw == 8) ? 512 : 256; }
+static int ap_emitted(int C, int ksize) { return ap_rows(C, ap_waves(C)) - 12 - (ksize - 1); }
 
 // x_next (or, last, the stage mean) of one AMPBlock1 half-layer pair; weights dense fp16 [C][kd] (hi plane at w1 / w2,
 // lo plane w_lo elements after it for F16W2), activation parameters as the fused epilogues take them
@@ -374,6 +394,7 @@ int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, 
   P.w1 = w1; P.w2 = w2; P.w_lo = w_lo;
   P.b1 = b1; P.b2 = b2; P.out_scale = out_scale; P.accumulate = last ? accumulate : 0;
   P.ae1 = ae1; P.ib1 = ib1; P.ae2 = ae2; P.ib2 = ib2; P.f1 = f1; P.f2 = f2;
+  P.ablate = knobs().ampair_ablate;
   const int E = ap_emitted(C, ksize);
   P.tiles_per_batch = (T + E - 1) / E;
   const int64_t nt = (int64_t)B * P.tiles_per_batch;
@@ -381,9 +402,10 @@ int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, 
   P.ntiles = (int)nt;
   void* tok = prof_start(s);
   int rc;
-  if (C == 24) rc = ap_by_k<24, 2, 512>(P, ksize, last, s);
-  else if (C == 48) rc = ap_by_k<48, 2, 256>(P, ksize, last, s);
-  else rc = ap_by_k<96, 1, 256>(P, ksize, last, s);
+  const int nw = ap_waves(C);
+  if (C == 24) rc = nw == 8 ? ap_by_k<24, 2, 512, 8, 24>(P, ksize, last, s) : ap_by_k<24, 2, 256, 4, 24>(P, ksize, last, s);
+  else if (C == 48) rc = nw == 8 ? ap_by_k<48, 2, 256, 8, 48>(P, ksize, last, s) : ap_by_k<48, 2, 256, 4, 24>(P, ksize, last, s);
+  else rc = ap_by_k<96, 1, 256, 8, 48>(P, ksize, last, s);
   if (rc) return rc;
   ALCM_HIP(hipGetLastError());
   if (tok) {

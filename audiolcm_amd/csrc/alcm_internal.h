@@ -130,6 +130,8 @@ struct Knobs {
   int ampair = 1;                // ALCM_AMPAIR: BigVGAN stages 3-5 as fused AMPBlock half-layer pairs (alcm_ampair.hip),
                                  // 0 = one launch per Activation1d / conv (tconv)
   int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
+  int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
+  int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
 };
 const Knobs& knobs();
 

@@ -54,6 +54,8 @@ static Knobs read_knobs() {
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   k.ampair = env_int("ALCM_AMPAIR", 1);
   k.ampair_grid = env_int("ALCM_AMPAIR_GRID", 0);
+  k.ampair_ablate = env_int("ALCM_AMPAIR_ABLATE", 0);
+  k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   return k;
 }
 
