@@ -53,6 +53,10 @@ int act_conv_post(const float* x, float* wav, int B, int T, int C, const float* 
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
+// Activation1d with both FIRs on MFMA, fp16 planes out (alcm_act.hip; C >= 192, C % 64 == 0, PREC_F16, Cp == C)
+bool act_mfma_ok(int C, int Cp, int prec);
+int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
+             const Taps12O& f, hipStream_t s);
 int nconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
@@ -132,6 +136,7 @@ struct Knobs {
   int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
   int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
   int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
+  int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
 };
 const Knobs& knobs();
 

@@ -112,6 +112,15 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   }
   const int64_t y_lo = (int64_t)B * T * Cp;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
+  if (act_mfma_ok(C, Cp, prec)) {  // both FIRs on MFMA (alcm_act.hip): the wide stages under the mixed policy
+    void* tok = prof_start(s);
+    ALCM_TRY(act_mfma(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
+    if (tok) {
+      const double e = (double)B * T;
+      prof_stop(tok, s, "alcm::act_mfma_kernel", 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp));
+    }
+    return 0;
+  }
   if (!knobs().act_v1) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
     void* tok = prof_start(s);
     ALCM_TRY(act_coop(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));

@@ -1,21 +1,34 @@
 #!/bin/bash
-# Round-4 GPU call: the new / changed GPU tests, then an A/B of the fused AMPBlock pair (ALCM_AMPAIR=1 default vs 0,
-# alternating in one call) on the default bench workload with per-kernel rows.  Usage: bash scripts/gpu_r4.sh <tag> [k]
+# Round-4 GPU call: selected GPU tests, optional microbench modes, then an A/B of knob settings on the default bench
+# workload (alternating, two rounds, per-kernel rows in the .err files).
+# Usage: bash scripts/gpu_r4.sh <tag> "<pytest -k expr>" "<microbench modes>" "<variant> ..."
+#   variant = a space-free env assignment list joined by commas, e.g. ALCM_AMPAIR=0,ALCM_ACT_MFMA=0 ("-" = defaults)
 tag=${1:-r4}
-sel=${2:-"ampblock or bigvgan or batch32 or rccl or world2 or bench_batch32"}
+sel=${2:-"ampblock or bigvgan or bench_batch32"}
+micro=${3:-""}
+variants=${4:-"- ALCM_AMPAIR=0"}
 out=gpurun_out/$tag; mkdir -p $out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "$sel" \
-  > $out/tests.log 2>&1
-rc=$?
-echo "TESTS EXIT $rc" >> $out/tests.log
-tail -3 $out/tests.log
-[ $rc -eq 0 ] || exit $rc
+if [ "$sel" != "none" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 400 --timeout-method thread -k "$sel" \
+    > $out/tests.log 2>&1
+  rc=$?
+  echo "TESTS EXIT $rc" >> $out/tests.log
+  grep -E "PASSED|FAILED|ERROR|passed|failed|act C|ampair C" $out/tests.log | tail -60
+  [ $rc -eq 0 ] || exit $rc
+fi
+for m in $micro; do
+  timeout -k 10 600 python -u scripts/microbench.py $m > $out/micro_$m.txt 2>&1 || exit $?
+  cat $out/micro_$m.txt
+done
 ARGS="--steps 5 --warmup 2 --also-other-mode 0 --cpu-baseline 0 --extra-configs 0 --components 0"
 for round in 1 2; do
-  for v in 1 0; do
-    ALCM_AMPAIR=$v ALCM_BENCH_ALL_KERNELS=1 timeout -k 10 300 python -u bench.py $ARGS \
-      > $out/ab_${round}_$v.json 2> $out/ab_${round}_$v.err || exit $?
-    echo "AMPAIR=$v: $(python -c "import json;d=json.load(open('$out/ab_${round}_$v.json'));print(d['value'], d['ms_per_step'])")" >> $out/ab.txt
+  for v in $variants; do
+    envs=""
+    [ "$v" != "-" ] && envs=$(echo "$v" | tr ',' ' ')
+    name=$(echo "$v" | tr ',=' '_-')
+    env $envs ALCM_BENCH_ALL_KERNELS=1 timeout -k 10 300 python -u bench.py $ARGS \
+      > $out/ab_${round}_$name.json 2> $out/ab_${round}_$name.err || exit $?
+    echo "$v: $(python -c "import json;d=json.load(open('$out/ab_${round}_$name.json'));print(d['value'], d['ms_per_step'])")" >> $out/ab.txt
   done
 done
 cat $out/ab.txt

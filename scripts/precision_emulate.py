@@ -48,12 +48,20 @@ def run(W, mel, policy, wscale=False):
         w_r = scaled_f16(w) if (w_f == "f16" and wscale) else rnd(w, w_f)
         return rnd(x, a_f), w_r
 
+    def fir(x, w, grp):  # Activation1d FIRs (depthwise): policy "fir" / "fir_<group>" = (input fmt, taps fmt)
+        a_f, w_f = policy.get(f"fir_{grp}", policy.get("fir", ("f32", "f32")))
+        return rnd(x, a_f), rnd(w, w_f)
+
     def conv1d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
         if groups == 1:
             x, w = q(x, w, state["group"])
+        else:
+            x, w = fir(x, w, state["group"])
         return real_conv(x, w, b, stride, padding, dilation, groups)
 
     def convt(x, w, b=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
+        if groups != 1:
+            x, w = fir(x, w, state["group"])
         if groups == 1:  # per-stage groups ups0 .. ups5 fall back to "ups"
             i = state["ups"] = state.get("ups", -1) + 1
             x, w = q(x, w, f"ups{i}" if f"ups{i}" in policy else "ups")
@@ -100,6 +108,15 @@ def main():
             "tail bf16": {"tail": ("bf16", "bf16")},
             "pre+ups+post bf16": {k: ("bf16", "bf16") for k in ("pre", "ups", "post")},
         }
+        if len(sys.argv) > 2 and sys.argv[2] == "fir":  # Activation1d FIRs on fp16 MFMA operands (mixed policy base)
+            wide_ups = {f"ups{i}": ("f16", "f16") for i in range(3)}
+            base = dict({"wide": ("f16", "f16"), "tail": ("f16", "f32"), "s3": ("f16", "f16")}, **wide_ups)
+            cases = {"mixed policy": base,
+                     "mixed + FIR inputs f16": dict(base, fir=("f16", "f32")),
+                     "mixed + FIR inputs+taps f16": dict(base, fir=("f16", "f16")),
+                     "mixed + wide FIR inputs f16": dict(base, fir_wide=("f16", "f32")),
+                     "mixed + tail FIR inputs f16": dict(base, **{f"fir_s{i}": ("f16", "f32") for i in (3, 4, 5)}),
+                     "mixed + FIR inputs bf16": dict(base, fir=("bf16", "f32"))}
         if len(sys.argv) > 2 and sys.argv[2] == "tail":  # per-stage weight rounding of the tail (mixed policy base)
             base = {"wide": ("f16", "f16"), "tail": ("f16", "f32")}
             cases = {"mixed (tail F16W2)": base}

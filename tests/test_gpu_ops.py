@@ -641,3 +641,30 @@ def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, monkeypatch):
     d = (y - ref).abs().max().item()
     print(f"ampair C{C} T{T} k{k} d{dil} {mode}: max |diff| {d:.3e} equal {torch.equal(y, ref)}")
     assert rel_l2(y.numpy(), ref.numpy()) < 2e-6
+
+
+@pytest.mark.parametrize("C,T", [(192, 37), (384, 300), (768, 2496), (192, 1000)])
+def test_activation1d_mfma(K, C, T, monkeypatch):
+    """Activation1d with both FIRs on MFMA (act_mfma_kernel: the wide stages under the mixed policy; fp16 FIR inputs,
+    taps split hi/lo) vs the fp32 oracle and vs the VALU kernel (ALCM_ACT_MFMA=0), on fp16 planes: within the fp16
+    rounding of the inputs (alias_free_torch/act.py:23-27).  T = 37 is one partial tile with both sequence ends."""
+    from audiolcm_amd import _hip
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    x = _r((2, C, T), 140, 1.5)
+    a, bt = _r((C,), 141, 0.3), _r((C,), 142, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    ref = O.activation1d(x, a, bt, f, f).permute(0, 2, 1).contiguous()
+    xd = dev(x.permute(0, 2, 1).contiguous())
+    got = K.activation1d_op(xd, dev(a), dev(bt), f, f, 2).cpu()[0].view(torch.float16).float()
+    monkeypatch.setenv("ALCM_ACT_MFMA", "0")
+    _hip.reload_knobs()
+    try:
+        valu = K.activation1d_op(xd, dev(a), dev(bt), f, f, 2).cpu()[0].view(torch.float16).float()
+    finally:
+        monkeypatch.delenv("ALCM_ACT_MFMA")
+        _hip.reload_knobs()
+    e_mfma, e_valu = rel_l2(got.numpy(), ref.numpy()), rel_l2(valu.numpy(), ref.numpy())
+    print(f"act C{C} T{T}: mfma {e_mfma:.2e} valu {e_valu:.2e} mfma-vs-valu {rel_l2(got.numpy(), valu.numpy()):.2e}")
+    assert torch.isfinite(got).all()
+    assert e_mfma < 1e-3 and e_mfma < 2.5 * e_valu
