@@ -137,6 +137,7 @@ struct Knobs {
   int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
   int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
+  int wconv3_flat = 1;           // ALCM_WCONV3_FLAT: wconv3 on padded-flat rows for under-filled clips (0 = wconv2)
 };
 const Knobs& knobs();
 

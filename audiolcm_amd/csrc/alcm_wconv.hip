@@ -42,6 +42,11 @@ struct WConvDev {
   int fpipe;            // wconv2: fragment-pipelined K loop (ALCM_WCONV_FPIPE)
   int ablate;           // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue,
                         // 2 no MFMA, 4 no global -> LDS staging in the K loop
+  // wconv3 FLAT (padded-flat rows): the B clips laid end to end with `pad` zero rows on each side of every clip
+  // (clip b row t = flat row b * flat_tp + pad + t, flat_tp = T + 2 pad, P.T = B * flat_tp), so 256-row tiles run
+  // full across clip boundaries (VAE: T = 312 would fill 2 tiles of 256 to 61 %); gap rows read zero, are not stored
+  int flat_tlen, flat_tp;
+  FastDiv flat_div;     // / flat_tp
 };
 
 
@@ -462,8 +467,9 @@ __device__ __forceinline__ void w3_quad_transpose(float (&v)[4], int q) {
 // up-projection's epilogue (new_attention.py:48-55): interleaved columns (2m, 2m+1) = (value m, gate m) ->
 // value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2].  EPI4: the fp32 epilogue with 16-B
 // accesses after an in-quad transpose (ALCM_W3_EPI=0: the 4-B column-access epilogue, A/B)
-template <int PREC, int AB, bool GEGLU = false, bool EPI4 = true>
+template <int PREC, int AB, bool GEGLU = false, bool EPI4 = true, bool FLAT = false>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
+  static_assert(!FLAT || (!GEGLU && !EPI4), "padded-flat rows: the 4-B fp32 epilogue");
   constexpr int TM = 4, TN = 6;
   constexpr bool ab_dma = (AB & 4) != 0, ab_sync = (AB & 16) != 0;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
@@ -512,8 +518,14 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   auto win_piece = [&](int j) {
     const int row = 8 * (wave + 8 * j) + (lane >> 3);
     const int ls = (lane & 7) ^ (row & 7);
-    const int ts = wrow0 + row;
-    const bool ok = row < WR && ts >= 0 && ts < P.T;
+    int ts = wrow0 + row;
+    bool ok = row < WR && ts >= 0 && ts < P.T;
+    if constexpr (FLAT) {  // padded-flat row -> (clip, row of the clip); the gap rows are zero
+      const int bq = (int)P.flat_div.div((uint32_t)max(ts, 0));
+      const int tt = ts - bq * P.flat_tp - P.pad;
+      ok = ok && tt >= 0 && tt < P.flat_tlen;
+      ts = bq * P.flat_tlen + tt;
+    }
     const u16* src = ok ? wsrc_base + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
     glds16(src, smem + wbuf * W3_WBUF + (wave + 8 * j) * 1024);
   };
@@ -747,10 +759,18 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           float rv[4][TN], pv[4][TN];
+          int orow[4];  // output row (b T + t) of each accumulator row, -1 where nothing is stored
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int t = min(t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r, P.T - 1);
-            const int64_t ro = ((int64_t)b * P.T + t) * P.N + col0 + wn * 96 + (lane & 15);
+            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            if constexpr (FLAT) {
+              const int bq = (int)P.flat_div.div((uint32_t)t);
+              const int tt = t - bq * P.flat_tp - P.pad;
+              orow[r] = (t < P.T && tt >= 0 && tt < P.flat_tlen) ? bq * P.flat_tlen + tt : -1;
+            } else {
+              orow[r] = t < P.T ? b * P.T + t : -1;
+            }
+            const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
               rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
@@ -759,9 +779,8 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-            if (t >= P.T) continue;
-            const int64_t ro = ((int64_t)b * P.T + t) * P.N + col0 + wn * 96 + (lane & 15);
+            if (orow[r] < 0) continue;
+            const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
@@ -789,7 +808,8 @@ static int g_ncu = 0;
 
 // Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
 // residual, scale, accumulate; no GEGLU / strided / fused activation).  Returns 1 when it launched.
-static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
+static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s,
+                      bool flat) {
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   const bool gl = a.geglu_plane != nullptr;
   if (a.out_act || a.out_stride > 0 || a.Cp % 64 || a.ksize < 3 || (a.ksize - 1) * a.dil > 64 || a.N % W3_BN ||
@@ -810,9 +830,18 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   P.gplane = (u16*)a.geglu_plane;
   P.fpipe = knobs().wconv3 == 2;  // wconv3: window DMA in one burst instead of spread over the chunk's steps
-  P.tiles_per_batch = (a.T + W3_BM - 1) / W3_BM;
+  int nb = a.B;
+  if (flat) {
+    P.flat_tlen = a.T;
+    P.flat_tp = a.T + 2 * a.pad;
+    P.flat_div = FastDiv((uint32_t)P.flat_tp);
+    if ((int64_t)a.B * P.flat_tp >= (1ll << 31)) return 0;
+    P.T = a.B * P.flat_tp;
+    nb = 1;
+  }
+  P.tiles_per_batch = (P.T + W3_BM - 1) / W3_BM;
   P.tiles_n = a.N / W3_BN;
-  const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
+  const int64_t nt = (int64_t)nb * P.tiles_per_batch * P.tiles_n;
   if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
   if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
   P.nwg = (int)nt;
@@ -833,6 +862,9 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   } else if (gl) {
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, true>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, true>), dim3(grid), dim3(512), 0, s, P);
+  } else if (flat) {
+    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, false, false, true>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, false, false, true>), dim3(grid), dim3(512), 0, s, P);
   } else if (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15)) {
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0>), dim3(grid), dim3(512), 0, s, P);
@@ -842,9 +874,9 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   }
   if (tok) {
     char name[96];
-    const bool e4 = gl || (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15));
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s>", a.prec, gl ? "true" : "false",
-                  e4 ? "true" : "false");
+    const bool e4 = !flat && (gl || (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15)));
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s%s>", a.prec, gl ? "true" : "false",
+                  e4 ? "true" : "false", flat ? ", true" : "");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -876,8 +908,14 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   // not for the GEGLU up-projection (its register epilogue evaluates erf on every lane: 5.25 vs 4.94 ms/step)
   const int w3 = knobs().wconv3;
   const int mt256 = (a.T + W3_BM - 1) / W3_BM;
-  if (!off && w3 != 0 && !act && !strided &&
-      (w3 > 0 || (a.T * 100 >= mt256 * W3_BM * 85 && !a.geglu_plane)) && wconv3_try(a, wplane, flops, bytes, s))
+  const bool full = a.T * 100 >= mt256 * W3_BM * 85;
+  // padded-flat rows (ALCM_WCONV3_FLAT, default on) where the per-clip 256-row tiles would be under 85 % full but the
+  // clips laid end to end fill them (the VAE's T = 312 / 624 k3 convs: 61 / 81 % -> 98 / 99 %)
+  const int64_t fr = (int64_t)a.B * (a.T + 2 * a.pad);
+  const bool flat = !full && !a.geglu_plane && a.B > 1 && knobs().wconv3_flat &&
+                    (int64_t)a.B * a.T * 100 >= (fr + W3_BM - 1) / W3_BM * W3_BM * 85;
+  if (!off && w3 != 0 && !act && !strided && (w3 > 0 || ((full || flat) && !a.geglu_plane)) &&
+      wconv3_try(a, wplane, flops, bytes, s, flat && !(w3 > 0 && full)))
     return 1;
   if (off && !act && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;

@@ -668,3 +668,38 @@ def test_activation1d_mfma(K, C, T, monkeypatch):
     print(f"act C{C} T{T}: mfma {e_mfma:.2e} valu {e_valu:.2e} mfma-vs-valu {rel_l2(got.numpy(), valu.numpy()):.2e}")
     assert torch.isfinite(got).all()
     assert e_mfma < 1e-3 and e_mfma < 2.5 * e_valu
+
+
+@pytest.mark.parametrize("C,N,T,k,B,grid", [(384, 384, 312, 3, 4, 0), (768, 768, 312, 3, 3, 8), (384, 192, 624, 5, 2, 0),
+                                            (192, 384, 100, 3, 7, 8)])
+def test_wconv3_padded_flat_rows(K, C, N, T, k, B, grid, monkeypatch):
+    """wconv3 on padded-flat rows (the VAE's under-filled clips, ldm/models/autoencoder1d.py:176-235): the B clips end
+    to end with (k-1)/2 zero rows between them, 256-row tiles across clip boundaries, gap rows neither read nor stored.
+    vs F.conv1d per clip, vs opconv_kernel (ALCM_WCONV=0) and vs the per-clip wide kernels (ALCM_WCONV3_FLAT=0): same
+    products, summation order differs only between kernels (fp32 rounding)."""
+    from audiolcm_amd import _hip
+    prec = 2
+    x = _r((B, T, C), 150)
+    w, bias = _r((N, C, k), 151, 0.7 / np.sqrt(C * k)), _r((N,), 152, 0.05)
+    r = _r((B, T, N), 153)
+    ref = (F.conv1d(x.permute(0, 2, 1), w, bias, padding=(k - 1) // 2).permute(0, 2, 1) + r) * 0.5 + 1.0
+    pl = K.operand_planes(dev(x), prec)
+
+    def run():
+        acc = dev(torch.ones((B, T, N)))
+        return K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r), out_scale=0.5, accumulate_into=acc).cpu()
+    outs = {}
+    for name, env in (("flat", {"ALCM_WCONV3_GRID": str(grid)}), ("opconv", {"ALCM_WCONV": "0"}),
+                      ("perclip", {"ALCM_WCONV3_FLAT": "0"})):
+        for kk, v in env.items():
+            monkeypatch.setenv(kk, v)
+        _hip.reload_knobs()
+        try:
+            outs[name] = run()
+        finally:
+            for kk in env:
+                monkeypatch.delenv(kk)
+            _hip.reload_knobs()
+    assert rel_l2(outs["flat"].numpy(), ref.numpy()) < TOL[prec]
+    assert rel_l2(outs["flat"].numpy(), outs["opconv"].numpy()) < 1e-5
+    assert rel_l2(outs["flat"].numpy(), outs["perclip"].numpy()) < 1e-5
