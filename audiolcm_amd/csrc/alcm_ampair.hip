@@ -329,7 +329,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
 
 // ------------------------------------------------------------------------------------------------------------- host
 bool ampair_supported(int prec, int C, int ksize, int dil) {
-  if (knobs().ampair == 0) return false;
   if (ksize != 3 && ksize != 7 && ksize != 11) return false;
   if (dil < 1 || dil > 5) return false;
   if (C == 96) return prec == PREC_F16;  // (the tail's F16W2-everywhere diagnostic keeps the unfused path)

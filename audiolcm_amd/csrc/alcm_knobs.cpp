@@ -52,7 +52,7 @@ static Knobs read_knobs() {
   k.text_gemm = env_set("ALCM_TEXT_GEMM");  // planes: 20.9 -> 13.5 ms per B = 32 text encode (profiles/r3f)
   k.sgemm = env_int("ALCM_SGEMM", 1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
-  k.ampair = env_int("ALCM_AMPAIR", 1);
+  k.ampair = env_int("ALCM_AMPAIR", 0);  // opt-in until it beats the unfused chain
   k.ampair_grid = env_int("ALCM_AMPAIR_GRID", 0);
   k.ampair_ablate = env_int("ALCM_AMPAIR_ABLATE", 0);
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);

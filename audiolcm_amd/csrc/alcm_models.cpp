@@ -1347,7 +1347,7 @@ static bool stage_tconv(const StageW& S, int prec) {
 // the narrow stages' AMPBlock half-layer pairs as one fused launch each (alcm_ampair.hip): every pair of the stage
 // or none
 static bool stage_ampair(const StageW& S, int prec) {
-  if (S.rb.empty() || !S.rb[0].c1[0].dw.p) return false;
+  if (!knobs().ampair || S.rb.empty() || !S.rb[0].c1[0].dw.p) return false;  // ALCM_AMPAIR=1: opt-in
   for (const AmpW& A : S.rb)
     for (size_t l = 0; l < A.dil.size(); ++l)
       if (!ampair_supported(prec, S.cout, A.k, A.dil[l]) || A.act.size() < 2 * A.dil.size()) return false;

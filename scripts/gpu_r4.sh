@@ -6,7 +6,7 @@
 tag=${1:-r4}
 sel=${2:-"ampblock or bigvgan or bench_batch32"}
 micro=${3:-""}
-variants=${4:-"- ALCM_AMPAIR=0"}
+variants=${4:-"- ALCM_AMPAIR=1"}
 out=gpurun_out/$tag; mkdir -p $out
 if [ "$sel" != "none" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 400 --timeout-method thread -k "$sel" \
