@@ -194,10 +194,12 @@ __device__ __forceinline__ uint32_t am_pair(float v) {  // (v, v) as two fp16
   return h | (h << 16);
 }
 
-__global__ __launch_bounds__(256) void act_mfma_kernel(const float* __restrict__ x, u16* __restrict__ y, int T, int C,
-                                                       int Cp, const float* __restrict__ aexp,
-                                                       const float* __restrict__ ibeta, const Taps12O f, int tiles_t,
-                                                       int tiles_c) {
+constexpr int AM_STRIP = 8;          // wave tiles per workgroup strip (the tap fragments are built once per strip)
+
+__global__ __launch_bounds__(256, 2) void act_mfma_kernel(const float* __restrict__ x, u16* __restrict__ y, int T,
+                                                          int C, int Cp, const float* __restrict__ aexp,
+                                                          const float* __restrict__ ibeta, const Taps12O f,
+                                                          int strips_t, int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
   __shared__ __attribute__((aligned(16))) uint32_t xs[4][16 * AM_XS];
   __shared__ __attribute__((aligned(16))) uint32_t ss[4][16 * AM_SS];
@@ -206,15 +208,15 @@ __global__ __launch_bounds__(256) void act_mfma_kernel(const float* __restrict__
   int bid = blockIdx.x;
   const int ct = bid % tiles_c;
   bid /= tiles_c;
-  const int tt = bid % tiles_t;
-  const int b = bid / tiles_t;
-  const int t0 = tt * AM_TT, c0 = ct * 64 + wave * 16;
-  if (c0 >= C) return;  // (C % 16 == 0: a wave is all in or all out; no workgroup barrier follows)
+  const int st = bid % strips_t;
+  const int b = bid / strips_t;
+  const int c0 = ct * 64 + wave * 16;
+  const int tile0 = st * AM_STRIP, ntile = min(AM_STRIP, (T + AM_TT - 1) / AM_TT - tile0);
   uint32_t* const xw = xs[wave];
   uint32_t* const sw = ss[wave];
 
-  // tap fragments: up A[q = l16][k = 8 q4 + e] = tap_(e&1)[ku], ku = q - 2 r' + 10, r' = 4 q4 + e / 2 (x row of the
-  // block); down B[k][n = l16] = tap_(e&1)[i' - 2 n], i' = 16 p + 4 q4 + e / 2 (sample of the block)
+  // tap fragments, once per strip: up A[q = l16][k = 8 q4 + e] = tap_(e&1)[ku], ku = q - 2 r' + 10, r' = 4 q4 + e / 2
+  // (x row of the block); down B[k][n = l16] = tap_(e&1)[i' - 2 n], i' = 16 p + 4 q4 + e / 2 (sample of the block)
   f16x8 aup, bdn[3];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -233,76 +235,92 @@ __global__ __launch_bounds__(256) void act_mfma_kernel(const float* __restrict__
       const _Float16 hi = (_Float16)tv;
       bdn[p][e] = (e & 1) ? (_Float16)(tv - (float)hi) : hi;
     }
-
-  // x rows t0 - 5 + r (clamped), channels c0 .. c0 + 15 -> (v, v) pairs at xw[c * XS + r]: lane = (row, channel quad)
-  const float* xb = x + (int64_t)b * T * C + c0 + (lane & 3) * 4;
-#pragma unroll
-  for (int it = 0; it < AM_XR / 16; ++it) {
-    const int r = it * 16 + (lane >> 2);
-    const int t = min(max(t0 - 5 + r, 0), T - 1);
-    const float4 v = *reinterpret_cast<const float4*>(xb + (int64_t)t * C);
-    const int c = (lane & 3) * 4;
-    xw[(c + 0) * AM_XS + r] = am_pair(v.x);
-    xw[(c + 1) * AM_XS + r] = am_pair(v.y);
-    xw[(c + 2) * AM_XS + r] = am_pair(v.z);
-    xw[(c + 3) * AM_XS + r] = am_pair(v.w);
-  }
   const int cl = c0 + l16;  // this lane's channel in the up products
   const float ear = aexp[cl] * INV_PI, hh = ibeta[cl] * 0.5f;
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's x pairs are in LDS
-  __builtin_amdgcn_wave_barrier();
 
-  // up blocks: samples i = 16 bk + 4 q4 + r of channel l16 -> SnakeBeta (fp32) -> (s, s) pairs at sw[l16 * SS + i]
+  // x rows t0 - 5 + r (clamped), channels c0 .. c0 + 15: lane = (row, channel quad); the next tile's rows are loaded
+  // into registers while this tile computes
+  const float* xb = x + (int64_t)b * T * C + c0 + (lane & 3) * 4;
+  float4 xv[AM_XR / 16];
+  auto load_x = [&](int t0) {
 #pragma unroll
-  for (int bk = 0; bk < AM_UPB; ++bk) {
-    const f16x8 bx = *reinterpret_cast<const f16x8*>(xw + l16 * AM_XS + 8 * bk + 4 * q4);
-    const f32x4 u = __builtin_amdgcn_mfma_f32_16x16x32_f16(aup, bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    uint4 o;
-    uint32_t* op = reinterpret_cast<uint32_t*>(&o);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float sv = fmaf(-hh, __builtin_amdgcn_cosf(u[r] * ear), u[r] + hh);
-      op[r] = am_pair(sv);
+    for (int it = 0; it < AM_XR / 16; ++it) {
+      const int t = min(max(t0 - 5 + it * 16 + (lane >> 2), 0), T - 1);
+      xv[it] = *reinterpret_cast<const float4*>(xb + (int64_t)t * C);
     }
-    *reinterpret_cast<uint4*>(sw + l16 * AM_SS + 16 * bk + 4 * q4) = o;
-  }
-  // DownSample1d replicate padding: samples m = 2 t0 - 5 + i outside [0, 2T) take s(0) / s(2T - 1)
-  const int i_lo = 5 - 2 * t0, i_hi = 2 * T + 4 - 2 * t0;  // local indices of m = 0 and m = 2T - 1
-  if (i_lo > 0 || i_hi < AM_UPB * 16 - 1) {
+  };
+  load_x(tile0 * AM_TT);
+  u16* yb = y + (int64_t)b * T * Cp + c0 + 4 * q4;
+  for (int tl = 0; tl < ntile; ++tl) {
+    const int t0 = (tile0 + tl) * AM_TT;
+    // (v, v) fp16 pairs at xw[c * XS + r]
+#pragma unroll
+    for (int it = 0; it < AM_XR / 16; ++it) {
+      const int r = it * 16 + (lane >> 2);
+      const int c = (lane & 3) * 4;
+      xw[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
+      xw[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
+      xw[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
+      xw[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+    }
+    if (tl + 1 < ntile) load_x(t0 + AM_TT);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's x pairs are in LDS (the prefetch stays in flight)
+    __builtin_amdgcn_wave_barrier();
+
+    // up blocks: samples i = 16 bk + 4 q4 + r of channel l16 -> SnakeBeta (fp32) -> (s, s) pairs at sw[l16 SS + i]
+#pragma unroll
+    for (int bk = 0; bk < AM_UPB; ++bk) {
+      const f16x8 bx = *reinterpret_cast<const f16x8*>(xw + l16 * AM_XS + 8 * bk + 4 * q4);
+      const f32x4 u = __builtin_amdgcn_mfma_f32_16x16x32_f16(aup, bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      uint4 o;
+      uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sv = fmaf(-hh, __builtin_amdgcn_cosf(u[r] * ear), u[r] + hh);
+        op[r] = am_pair(sv);
+      }
+      *reinterpret_cast<uint4*>(sw + l16 * AM_SS + 16 * bk + 4 * q4) = o;
+    }
+    // DownSample1d replicate padding: samples m = 2 t0 - 5 + i outside [0, 2T) take s(0) / s(2T - 1)
+    const int i_lo = 5 - 2 * t0, i_hi = 2 * T + 4 - 2 * t0;  // local indices of m = 0 and m = 2T - 1
+    if (i_lo > 0 || i_hi < AM_UPB * 16 - 1) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (q4 == 0) {
+        uint32_t* row = sw + l16 * AM_SS;
+        if (i_lo > 0) {
+          const uint32_t v0 = row[i_lo];
+          for (int i = 0; i < i_lo; ++i) row[i] = v0;
+        }
+        if (i_hi >= 0 && i_hi < AM_UPB * 16 - 1) {
+          const uint32_t v1 = row[i_hi];
+          for (int i = i_hi + 1; i < AM_UPB * 16; ++i) row[i] = v1;
+        }
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    if (q4 == 0) {
-      uint32_t* row = sw + l16 * AM_SS;
-      if (i_lo > 0) {
-        const uint32_t v0 = row[i_lo];
-        for (int i = 0; i < i_lo; ++i) row[i] = v0;
-      }
-      if (i_hi >= 0 && i_hi < AM_UPB * 16 - 1) {
-        const uint32_t v1 = row[i_hi];
-        for (int i = i_hi + 1; i < AM_UPB * 16; ++i) row[i] = v1;
-      }
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
 
-  // down blocks: outputs j = t0 + 16 d + l16, channels c0 + 4 q4 .. + 3 -> 8-B fp16 plane stores
-  u16* yb = y + (int64_t)b * T * Cp + c0 + 4 * q4;
+    // down blocks: outputs j = t0 + 16 d + l16, channels c0 + 4 q4 .. + 3 -> 8-B fp16 plane stores
 #pragma unroll
-  for (int d = 0; d < AM_TT / 16; ++d) {
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < AM_TT / 16; ++d) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const f16x8 a = *reinterpret_cast<const f16x8*>(sw + l16 * AM_SS + 32 * d + 16 * p + 4 * q4);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bdn[p], acc, 0, 0, 0);
+      for (int p = 0; p < 3; ++p) {
+        const f16x8 a = *reinterpret_cast<const f16x8*>(sw + l16 * AM_SS + 32 * d + 16 * p + 4 * q4);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bdn[p], acc, 0, 0, 0);
+      }
+      const int j = t0 + 16 * d + l16;
+      if (j < T) {
+        uint2 w;
+        w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
+        w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
+        *reinterpret_cast<uint2*>(yb + (int64_t)j * Cp) = w;
+      }
     }
-    const int j = t0 + 16 * d + l16;
-    if (j < T) {
-      uint2 w;
-      w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
-      w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
-      *reinterpret_cast<uint2*>(yb + (int64_t)j * Cp) = w;
-    }
+    // the next tile's x pairs overwrite xw only after this tile's up reads retired (same wave, in order)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -314,10 +332,11 @@ int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* 
              const Taps12O& f, hipStream_t s) {
   if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 7)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
   const int tiles_t = (T + AM_TT - 1) / AM_TT, tiles_c = C / 64;
-  const int64_t nwg = (int64_t)B * tiles_t * tiles_c;
+  const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
+  const int64_t nwg = (int64_t)B * strips_t * tiles_c;
   if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma: too large");
   hipLaunchKernelGGL(act_mfma_kernel, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp, inv_beta,
-                     f, tiles_t, tiles_c);
+                     f, strips_t, tiles_c);
   ALCM_HIP(hipGetLastError());
   return 0;
 }

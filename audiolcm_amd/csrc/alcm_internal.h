@@ -138,6 +138,7 @@ struct Knobs {
   int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int wconv3_flat = 1;           // ALCM_WCONV3_FLAT: wconv3 on padded-flat rows for under-filled clips (0 = wconv2)
+  int wconv4 = 1;                // ALCM_WCONV4: wconv3 with the tap loop unrolled at compile time (0 = wconv3)
 };
 const Knobs& knobs();
 

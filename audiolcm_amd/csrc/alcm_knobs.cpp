@@ -58,6 +58,7 @@ static Knobs read_knobs() {
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.wconv3_flat = env_int("ALCM_WCONV3_FLAT", 1);
+  k.wconv4 = env_int("ALCM_WCONV4", 0);
   return k;
 }
 

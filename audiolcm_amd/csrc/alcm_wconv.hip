@@ -804,6 +804,244 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// wconv4: wconv3's tile, LDS images, fragment pipeline and epilogue with the tap loop unrolled at compile time
+// (KS = 3 / 5 / 7 / 9 / 11).  Per step, everything wconv3 decides at run time is then a constant of the unrolled
+// code: whether the step ends a chunk, which window pieces it issues and so the counted vmcnt of its mid-step wait,
+// the next step's tap, and whether the weight step it issues 3 ahead lies in this chunk or the next one (two bases
+// per chunk instead of the per-step cursor with its chunk / tile switches).  Chunk and tile bookkeeping runs once
+// per chunk.  Past the last step the kernel re-issues valid addresses (the loads land in buffers nobody reads) so the
+// counted waits stay exact.  Bit-identical to wconv3 (same products in the same order).
+template <int I, int N, class F>
+__device__ __forceinline__ void w4_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    w4_static_for<I + 1, N>(f);
+  }
+}
+
+template <int PREC, int KS, bool FLAT>
+__global__ __launch_bounds__(512, 1) void wconv4_kernel(const WConvDev P) {
+  constexpr int TM = 4, TN = 6;
+  static_assert(KS >= 3, "three weight steps in flight");
+  constexpr int WSP = KS - 2;  // window pieces of the next chunk spread over taps < min(WSP, W3_WPW)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  const int ntiles = P.nwg;
+  const int R8 = (ntiles + 7) >> 3;
+  const int tbeg = xcd * R8, tend = min(tbeg + R8, ntiles);
+  const int first = tbeg + slot;
+  const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
+  if (my_n == 0) return;
+  const int Cp = P.Cp, nC = Cp / 64, dil = P.dil;
+  const int WR = W3_BM + (KS - 1) * dil;
+  const int tiles_m = ntiles / P.tiles_n;
+  auto tile_of = [&](int ti, int& b, int& t0, int& col0) {
+    const int tile = first + min(ti, my_n - 1) * nslot;  // (clamped: past the last tile, re-point at it)
+    int mt, nt;
+    if (P.n_major) {
+      nt = tile / tiles_m;
+      mt = tile - nt * tiles_m;
+    } else {
+      mt = tile / P.tiles_n;
+      nt = tile - mt * P.tiles_n;
+    }
+    b = mt / P.tiles_per_batch;
+    t0 = (mt - b * P.tiles_per_batch) * W3_BM;
+    col0 = nt * W3_BN;
+  };
+  // window of chunk (ti, c) -> buffer wb: W3_WPW DMA instructions of 8 rows x 128 B per wave
+  const u16* wsrc = P.a;
+  int wrow0 = 0;
+  auto win_setup = [&](int ti, int c) {
+    int b, t0, col0;
+    tile_of(ti, b, t0, col0);
+    wsrc = P.a + (int64_t)b * P.T * Cp + c * 64;
+    wrow0 = t0 - P.pad;
+  };
+  auto win_piece = [&](int j, int wb) {
+    const int row = 8 * (wave + 8 * j) + (lane >> 3);
+    const int ls = (lane & 7) ^ (row & 7);
+    int ts = wrow0 + row;
+    bool ok = row < WR && ts >= 0 && ts < P.T;
+    if constexpr (FLAT) {
+      const int bq = (int)P.flat_div.div((uint32_t)max(ts, 0));
+      const int tt = ts - bq * P.flat_tp - P.pad;
+      ok = ok && tt >= 0 && tt < P.flat_tlen;
+      ts = bq * P.flat_tlen + tt;
+    }
+    const u16* src = ok ? wsrc + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
+    glds16(src, smem + wb * W3_WBUF + (wave + 8 * j) * 1024);
+  };
+  uint32_t boff[W3_BPW];
+#pragma unroll
+  for (int j = 0; j < W3_BPW; ++j) {
+    const int n = 8 * (wave + 8 * j) + (lane >> 3);
+    boff[j] = (uint32_t)(n * P.kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
+  }
+  auto issue_wt = [&](int64_t off, int sl) {  // weight step at element offset `off` -> ring slot sl
+    const char* base = reinterpret_cast<const char*>(P.w + off);
+#pragma unroll
+    for (int j = 0; j < W3_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 8 * j) * 1024);
+  };
+  auto wbase = [&](int ti, int c) -> int64_t {  // weight element offset of (tile ti, chunk c, tap 0)
+    int b, t0, col0;
+    tile_of(ti, b, t0, col0);
+    return (int64_t)col0 * P.kpad + c * 64;
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow0 = wm * 64 + (lane & 15);
+  const int nrow0 = wn * 96 + (lane & 15);
+  const int bsw = lane & 7;
+  auto rdA = [&](int buf, int tp, int sub, int i) -> bf16x8 {
+    int arow = arow0 + tp * dil;
+    asm volatile("" : "+v"(arow));  // recomputed per read: hoisting KS per-tap addresses out of the chunk loop spills
+    return *reinterpret_cast<const bf16x8*>(smem + buf * W3_WBUF + arow * 128 +
+                                            (((4 * sub + (lane >> 4)) ^ (arow & 7)) << 4) + i * 16 * 128);
+  };
+  auto rdB = [&](int sl, int sub, int j) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(smem + 2 * W3_WBUF + sl * W3_BBUF + nrow0 * 128 +
+                                            (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
+  };
+
+  // prologue: window (0, 0); weight steps 0, 1, 2 (all in chunk 0: KS >= 3)
+  int64_t wb_cur = wbase(0, 0);
+  win_setup(0, 0);
+#pragma unroll
+  for (int j = 0; j < W3_WPW; ++j) win_piece(j, 0);
+  issue_wt(wb_cur, 0);
+  issue_wt(wb_cur + Cp, 1);
+  issue_wt(wb_cur + 2 * Cp, 2);
+  w3_wait_barrier<2 * W3_BPW>();
+  bf16x8 aA[TM], aB[TM], bA[TN], bB[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) aA[i] = rdA(0, 0, 0, i);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
+
+  int sl = 0;   // ring slot of the current step
+  int q = 0;    // global chunk: window buffer q & 1
+  for (int ti = 0; ti < my_n; ++ti) {
+    for (int c = 0; c < nC; ++c, ++q) {
+      // the chunk after this one (the next tile's first, or past the end: this one again)
+      const bool last_c = c + 1 == nC;
+      const int nti = last_c ? ti + 1 : ti, nc = last_c ? 0 : c + 1;
+      const int64_t wb_next = (nti < my_n) ? wbase(nti, nc) : wb_cur;
+      const int wbuf = q & 1;
+      w4_static_for<0, KS>([&](auto tap_c) {
+        constexpr int tap = decltype(tap_c)::value;
+        // ---- slice 0 on (aA, bA); slice 1's fragments read under it
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
+          if (i == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
+#pragma unroll
+            for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(wbuf, tap, 1, ii);
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
+        __builtin_amdgcn_s_setprio(0);
+        // ---- mid-step: weight step g + 1 resident (and, at the chunk's last tap, the next chunk's window: its
+        //      pieces went out at taps <= KS - 3, before weight step g + 1); what the previous mid-step issued and
+        //      weight step g + 2 stay in flight
+        constexpr int prev = tap == 0 ? 0 : (tap - 1 < WSP && tap - 1 < W3_WPW ? (W3_WPW - (tap - 1) + WSP - 1) / WSP : 0);
+        w3_wait_barrier<W3_BPW + prev>();
+        if constexpr (tap < WSP && tap < W3_WPW) {
+          if constexpr (tap == 0) {
+            if (nti < my_n) win_setup(nti, nc);  // (no next chunk: re-stage this one into the idle buffer)
+          }
+#pragma unroll
+          for (int j = tap; j < W3_WPW; j += WSP) win_piece(j, wbuf ^ 1);
+        }
+        // ---- slice 1 on (aB, bB); the next step's slice-0 fragments read under it; weight step g + 3 issued into
+        //      the slot this step has finished reading
+        const int sl1 = sl == 2 ? 0 : sl + 1;
+        constexpr bool cend = tap == KS - 1;
+        const int nbuf = cend ? wbuf ^ 1 : wbuf;
+        constexpr int ntap = cend ? 0 : tap + 1;
+        const int64_t woff = (tap + 3 < KS) ? wb_cur + (tap + 3) * Cp : wb_next + (tap + 3 - KS) * Cp;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+          if (i == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+#pragma unroll
+            for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+            issue_wt(woff, sl);
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+        __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
+        __builtin_amdgcn_s_setprio(0);
+        sl = sl1;
+        __builtin_amdgcn_sched_barrier(0);  // no code motion across steps (live ranges of the unrolled taps)
+      });
+      wb_cur = wb_next;
+    }
+    // ---- tile epilogue from the accumulators: out = (acc + bias + res) * scale (+ out)
+    {
+      int b, t0, col0;
+      tile_of(ti, b, t0, col0);
+      float bv[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float rv[4][TN], pv[4][TN];
+        int orow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          if constexpr (FLAT) {
+            const int bq = (int)P.flat_div.div((uint32_t)t);
+            const int tt = t - bq * P.flat_tp - P.pad;
+            orow[r] = (t < P.T && tt >= 0 && tt < P.flat_tlen) ? bq * P.flat_tlen + tt : -1;
+          } else {
+            orow[r] = t < P.T ? b * P.T + t : -1;
+          }
+          const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
+            pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (orow[r] < 0) continue;
+          const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
 static int g_ncu = 0;
 
 // Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
@@ -852,7 +1090,28 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
   const int ab = knobs().wconv_ablate;
-  if (ab && a.prec == PREC_F16) {
+  const bool e4req = knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15);
+  const int ks = a.ksize;
+  const bool w4 = knobs().wconv4 && !gl && !ab && (flat || !e4req) && (ks == 3 || ks == 5 || ks == 7 || ks == 9 || ks == 11);
+  if (w4) {
+    auto go4 = [&](auto kc, auto fc) {
+      constexpr int KSC = decltype(kc)::value;
+      constexpr bool FL = decltype(fc)::value;
+      if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv4_kernel<PREC_F16, KSC, FL>), dim3(grid), dim3(512), 0, s, P);
+      else hipLaunchKernelGGL((wconv4_kernel<PREC_BF16, KSC, FL>), dim3(grid), dim3(512), 0, s, P);
+    };
+    auto byk = [&](auto fc) {
+      switch (ks) {
+        case 3: go4(std::integral_constant<int, 3>{}, fc); break;
+        case 5: go4(std::integral_constant<int, 5>{}, fc); break;
+        case 7: go4(std::integral_constant<int, 7>{}, fc); break;
+        case 9: go4(std::integral_constant<int, 9>{}, fc); break;
+        default: go4(std::integral_constant<int, 11>{}, fc); break;
+      }
+    };
+    if (flat) byk(std::true_type{});
+    else byk(std::false_type{});
+  } else if (ab && a.prec == PREC_F16) {
     switch (ab) {
 #define W3AB(v) case v: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, v>), dim3(grid), dim3(512), 0, s, P); break;
       W3AB(1) W3AB(4) W3AB(5) W3AB(21)
@@ -874,9 +1133,12 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   }
   if (tok) {
     char name[96];
-    const bool e4 = !flat && (gl || (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15)));
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s%s>", a.prec, gl ? "true" : "false",
-                  e4 ? "true" : "false", flat ? ", true" : "");
+    const bool e4 = !flat && (gl || e4req);
+    if (w4)
+      std::snprintf(name, sizeof(name), "alcm::wconv4_kernel<%d, %d, %s>", a.prec, ks, flat ? "true" : "false");
+    else
+      std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s%s>", a.prec, gl ? "true" : "false",
+                    e4 ? "true" : "false", flat ? ", true" : "");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);

@@ -703,3 +703,33 @@ def test_wconv3_padded_flat_rows(K, C, N, T, k, B, grid, monkeypatch):
     assert rel_l2(outs["flat"].numpy(), ref.numpy()) < TOL[prec]
     assert rel_l2(outs["flat"].numpy(), outs["opconv"].numpy()) < 1e-5
     assert rel_l2(outs["flat"].numpy(), outs["perclip"].numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("C,T,k,dil,B,grid", [(768, 600, 11, 5, 2, 8), (384, 1100, 7, 3, 2, 0), (192, 1500, 3, 1, 2, 16),
+                                              (576, 467, 9, 1, 2, 0), (384, 312, 3, 1, 4, 0), (384, 624, 5, 1, 2, 8)])
+def test_wconv4_compile_time_taps(K, C, T, k, dil, B, grid, monkeypatch):
+    """wconv4 (wconv3 with the tap loop unrolled at compile time, ALCM_WCONV4=1) == wconv3 bit for bit (same products
+    in the same order), per-clip and padded-flat rows, one or several tiles per workgroup; and vs F.conv1d."""
+    from audiolcm_amd import _hip
+    prec = 2
+    x = _r((B, T, C), 160)
+    w, bias = _r((C, C, k), 161, 0.7 / np.sqrt(C * k)), _r((C,), 162, 0.05)
+    r = _r((B, T, C), 163)
+    ref = (F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1) + r) * 0.5
+    pl = K.operand_planes(dev(x), prec)
+    outs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("ALCM_WCONV4", v)
+        monkeypatch.setenv("ALCM_WCONV3", "1")
+        monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
+        _hip.reload_knobs()
+        try:
+            acc = dev(torch.ones((B, T, C)))
+            outs.append(K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=0.5,
+                                 accumulate_into=acc).cpu() - 1)
+        finally:
+            for kk in ("ALCM_WCONV4", "ALCM_WCONV3", "ALCM_WCONV3_GRID"):
+                monkeypatch.delenv(kk)
+            _hip.reload_knobs()
+    assert torch.equal(outs[0], outs[1])
+    assert rel_l2(outs[0].numpy(), ref.numpy()) < TOL[prec]
