@@ -10,8 +10,9 @@
 // range, so neighbouring tiles' halo rows are shared in its L2).  Per tile, with conv rows [s1, s1 + CR):
 //   1. act1: x rows [s1 - p1 - 6, s1 + CR + p1 + 6) (global, fp32) -> fp16 operand rows a1 [s1 - p1, s1 + CR + p1)
 //      in LDS (rows outside [0, T): zeros = conv1's zero padding; replicate padding near the ends as clamped reads);
-//   2. conv1 (dense K = tap * C + c, weights streamed per 32-deep slice through a 3-slot LDS ring by LDS-DMA, two
-//      slices in flight across phases and tiles) -> acc + bias staged in LDS (fp32, <= 48 channels per group);
+//   2. conv1 (dense K = tap * C + c; weights by LDS-DMA, resident for the launch (C = 24), one conv resident and
+//      swapped under the other phase (C = 48) or streamed per 32-deep slice through a ring (C = 96)) -> acc + bias
+//      staged in LDS (fp32, one channel group at a time);
 //   3. act2 from the staged rows -> fp16 operand rows a2 [s1 + 6, s1 + CR - 6) over the dead a1 rows;
 //   4. conv2 over a2 -> + bias + residual (prefetched during act2) -> x_next rows [e0, e0 + E), e0 = s1 + 6 + (k-1)/2,
 //      or for a resblock's last pair the stage mean: out = x_next * out_scale (+ out).
@@ -53,7 +54,7 @@ struct APairDev {
                // 8 no output stores
 };
 
-template <int C, int NPB, int KS, int CR, int NW_, int V1C_>
+template <int C, int NPB, int KS, int CR, int NW_, int V1C_, int WM_, int RD_>
 struct APairGeo {
   static constexpr int NW = NW_, NT = NW * 64;
   static constexpr int TM = CR / 16 / NW;                 // 16-row M tiles per wave
@@ -70,13 +71,22 @@ struct APairGeo {
   static constexpr int V1B = (CR * V1S * 4 + 1023) / 1024 * 1024;
   static constexpr int KD = (KS * C + 31) / 32 * 32;      // dense K
   static constexpr int NS = KD / 32;                      // slices per conv
-  static constexpr int SLOT = NSP * 64 * NPB;             // one 32-deep slice of every weight plane
+  // weight modes: WM 0 streams 32-deep slices of both convs through a ring of RD + 1 slots (RD slices in flight
+  // across phases and tiles); WM 1 keeps both convs' weights resident for the whole launch; WM 2 keeps one conv's
+  // resident and swaps it under the other phase (W2 loads under act2, the next tile's W1 under the epilogue + act1)
+  static constexpr int WM = WM_, RD = RD_, RING = RD + 1;
+  static constexpr int SLOT = NSP * 64 * NPB;             // ring: one 32-deep slice of every weight plane
   static constexpr int SPI = SLOT / 1024;                 // DMA instructions per slice
   static constexpr int DPW = (SPI + NW - 1) / NW;         // per wave (uniform: surplus lanes write the scratch line)
-  static constexpr int RING = 3;                          // slice s + 2 is issued into the slot slice s - 1 used
-  static constexpr int SMEM = A1B + V1B + RING * SLOT + 1024;
+  static constexpr int WSL = (KD / 8) % 2 ? KD / 8 : KD / 8 + 1;  // resident: weight row of an odd number of 16-B
+  static constexpr int WRS = WSL * 16;                             // slots (conflict-free 16-row fragment reads)
+  static constexpr int WCONV = NPB * NSP * WRS;           // one conv's resident planes [plane][row][K]
+  static constexpr int WCR = (WCONV + 1023) / 1024 * 1024;
+  static constexpr int WB = WM == 0 ? RING * SLOT + 1024 : (WM == 1 ? 2 : 1) * WCR;
+  static constexpr int SMEM = A1B + V1B + WB;
   static_assert(C % 16 == 8 || C % 16 == 0, "C % 8");
   static_assert(CR % (16 * NW) == 0 && SLOT % 1024 == 0 && C % V1C == 0 && V1C % 2 == 0, "geometry");
+  static_assert(WM == 0 ? (RD >= 2 && (RD - 1) * DPW < 64) : RD == 0, "ring depth");
   static_assert(SMEM <= (NW == 4 ? 81920 : 163840), "LDS (4 waves: two workgroups per CU)");
 };
 
@@ -146,16 +156,16 @@ __device__ __forceinline__ void ap_act(int n, int t_org, int T, const Taps12O& f
   }
 }
 
-template <int C, int NPB, int KS, int CR, int NW, int V1C_, int R, bool LAST>
+template <int C, int NPB, int KS, int CR, int NW, int V1C_, int WM, int RD, int R, bool LAST>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const APairDev P) {
-  using G = APairGeo<C, NPB, KS, CR, NW, V1C_>;
+  using G = APairGeo<C, NPB, KS, CR, NW, V1C_, WM, RD>;
   constexpr int NT = G::NT, TM = G::TM, TN = G::TN, NSP = G::NSP, RS = G::RS, NS = G::NS;
   constexpr int E = G::E, P2 = G::P2, V1C = G::V1C, V1S = G::V1S, SLOT = G::SLOT;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   char* const abuf = smem;                                         // a1, then a2
   float* const v1 = reinterpret_cast<float*>(smem + G::A1B);       // staged conv1 output (one channel group)
-  char* const ring = smem + G::A1B + G::V1B;
-  char* const scratch = ring + G::RING * SLOT;
+  char* const wbuf = smem + G::A1B + G::V1B;                       // weight ring (WM 0) or resident weights
+  char* const scratch = wbuf + G::RING * SLOT;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q4 = lane >> 4, l16 = lane & 15;
@@ -167,15 +177,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
   const int tbeg = xcd * R8 + slot, tend = min(xcd * R8 + R8, P.ntiles);
   const int my_n = tbeg < tend ? (tend - tbeg + nslot - 1) / nslot : 0;
   if (my_n == 0) return;
-  const int total = my_n * 2 * NS;  // weight slices this workgroup streams
+  const int total = my_n * 2 * NS;  // WM 0: weight slices this workgroup streams
 
-  // weight slice gs (tile gs / (2 NS), conv (gs / NS) & 1, slice gs % NS) -> ring slot gs % RING; instruction
+  // WM 0: weight slice gs (tile gs / (2 NS), conv (gs / NS) & 1, slice gs % NS) -> ring slot gs % RING; instruction
   // i = wave + NW j covers bytes [1024 i, 1024 i + 1024) of the slot: [plane][row n of 64 B][piece], the 16-B piece
   // pq of row n holding K piece pq ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows)
   auto issue = [&](int gs) {
     const int sl = gs % NS;
     const u16* wb = ((gs / NS) & 1) ? P.w2 : P.w1;
-    char* dst = ring + (gs % G::RING) * SLOT;
+    char* dst = wbuf + (gs % G::RING) * SLOT;
 #pragma unroll
     for (int j = 0; j < G::DPW; ++j) {
       const int i = wave + G::NW * j;
@@ -188,15 +198,35 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
       ap_glds16(src, i < G::SPI ? dst + i * 1024 : scratch);
     }
   };
-  issue(0);
-  if (total > 1) issue(1);
+  // WM 1 / 2: one conv's weights -> resident image [plane][row n (WRS bytes)][K], lane-linear 1 KB DMA instructions
+  // (rows >= C, the odd-slot pad and the last instruction's tail: zeros / the region's padding)
+  auto load_w = [&](const u16* wsrc, char* dst) {
+    constexpr int NI = G::WCR / 1024;
+    for (int i = wave; i < NI; i += NW) {
+      const int o = i * 1024 + lane * 16;
+      const int p = o / (NSP * G::WRS), r = o - p * (NSP * G::WRS);
+      const int n = r / G::WRS, qq = (r - n * G::WRS) >> 4;
+      const bool ok = o < G::WCONV && n < C && qq < G::KD / 8;
+      const u16* src = ok ? wsrc + p * P.w_lo + n * G::KD + qq * 8 : reinterpret_cast<const u16*>(g_ampair_zero);
+      ap_glds16(src, dst + i * 1024);
+    }
+  };
+  if constexpr (WM == 0) {
+#pragma unroll
+    for (int d = 0; d < RD; ++d)
+      if (d < total) issue(d);
+  } else {
+    load_w(P.w1, wbuf);
+    if constexpr (WM == 1) load_w(P.w2, wbuf + G::WCR);
+  }
 
   const int bsw = (l16 >> 2) & 3;
   f32x4 acc[TM][TN];
-  // one conv's K loop: slices gs0 .. gs0 + NS - 1 over the operand rows `a` (row of M tile i of this wave for tap t:
-  // wave * TM * 16 + i * 16 + l16 + t * dl); slice gs + 2 is issued into the slot slice gs - 1 used, one barrier per
-  // slice behind a counted wait that leaves that slice in flight
-  auto kloop = [&](const char* a, int dl, int gs0) {
+  // one conv's K loop over the operand rows `a` (row of M tile i of this wave for tap t: wave * TM * 16 + i * 16 +
+  // l16 + t * dl).  WM 0: slices gs0 .. gs0 + NS - 1 from the ring; slice gs + RD is issued into the slot slice
+  // gs - 1 used, one barrier per slice behind a counted wait that leaves the younger slices in flight.  WM 1 / 2:
+  // straight from the resident image (no waits, no barriers)
+  auto kloop = [&](const char* a, int dl, int conv, int gs0) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -205,18 +235,24 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int gs = gs0 + s;
-      const bool more = gs + 2 < total;
-      if (more) issue(gs + 2);
+      const bool more = WM == 0 && gs + RD < total;
       const int kk = s * 32 + q4 * 8;
       int tap = kk / C;
       const int c = kk - tap * C;
       tap = min(tap, KS - 1);  // K padding: zero weights, any finite operand row
-      const char* bs = ring + (gs % G::RING) * SLOT + l16 * 64 + ((q4 ^ bsw) << 4);
+      constexpr int BJ = WM == 0 ? 16 * 64 : 16 * G::WRS, BP = WM == 0 ? NSP * 64 : NSP * G::WRS;
+      const char* bs;
+      if constexpr (WM == 0) {
+        if (more) issue(gs + RD);
+        bs = wbuf + (gs % G::RING) * SLOT + l16 * 64 + ((q4 ^ bsw) << 4);
+      } else {
+        bs = wbuf + (WM == 1 ? conv * G::WCR : 0) + l16 * G::WRS + kk * 2;
+      }
       bf16x8 af[TM], bh[TN], bl[NPB == 2 ? TN : 1];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(bs + j * 16 * 64);
-        if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bs + NSP * 64 + j * 16 * 64);
+        bh[j] = *reinterpret_cast<const bf16x8*>(bs + j * BJ);
+        if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bs + BP + j * BJ);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dl) * RS + c * 2);
@@ -234,8 +270,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
             acc[i][j] = mfma16<PREC_F16>(af[i], bh[j], acc[i][j]);
           }
       }
-      if (more) ap_wait_barrier<G::DPW>();
-      else ap_wait_barrier<0>();
+      if constexpr (WM == 0) {
+        if (more) ap_wait_barrier<(RD - 1) * G::DPW>();
+        else ap_wait_barrier<0>();
+      }
     }
   };
 
@@ -254,10 +292,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
                                 return *reinterpret_cast<const f32x2*>(
                                     reinterpret_cast<const char*>(xb) + (uint32_t)(i * C + 2 * p) * 4u);
                               });
-    ap_wait_barrier<G::DPW>();  // slice gs0 resident for every wave (gs0 + 1 may stay in flight); a1 complete
+    // a1 complete; WM 0: slice gs0 resident for every wave (younger slices may stay in flight); WM 1 / 2: W1 resident
+    if constexpr (WM == 0) ap_wait_barrier<(RD - 1) * G::DPW>();
+    else ap_wait_barrier<0>();
 
     // ---- 2. conv1
-    kloop(abuf, P.dil, gs0);
+    kloop(abuf, P.dil, 0, gs0);
 
     float rv[TM][TN][4];
     // ---- 3. act2 per channel group: conv1 + bias -> LDS, then Activation1d -> a2 rows [s1 + 6, s1 + CR - 6)
@@ -276,6 +316,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
           }
         }
       __syncthreads();
+      if constexpr (WM == 2)
+        if (g == 0) load_w(P.w2, wbuf);  // every wave is past conv1: W2 over W1, under act2
       if (g == G::NG - 1) {
         // residual rows of this wave's conv2 outputs (row e0 + wave TM 16 + 16 i + 4 q4 + r, column 16 j + l16),
         // loaded under the last group's act2 (the accumulators are dead by then: no register overlap)
@@ -298,11 +340,17 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
                                   [&](int i, int p) {  // (rows past the staged tile: a partial run's unused tail)
                                     return *reinterpret_cast<const f32x2*>(v1 + min(i - s1, CR - 1) * V1S + 2 * p);
                                   });
-      __syncthreads();
+      if (WM == 2 && g == G::NG - 1) ap_wait_barrier<0>();  // a2 complete, W2 resident
+      else __syncthreads();
     }
 
     // ---- 4. conv2 + bias + residual -> out
-    kloop(abuf, 1, gs0 + NS);
+    kloop(abuf, 1, 1, gs0 + NS);
+    if constexpr (WM != 0) {
+      __syncthreads();  // every wave is past conv2 (a2 / W2 reads) before act1 / the W1 reload overwrite them
+      if constexpr (WM == 2)
+        if (it + 1 < my_n) load_w(P.w1, wbuf);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -337,9 +385,9 @@ bool ampair_supported(int prec, int C, int ksize, int dil) {
 
 static int g_ap_ncu = 0;
 
-template <int C, int NPB, int KS, int CR, int NW, int V1C>
+template <int C, int NPB, int KS, int CR, int NW, int V1C, int WM, int RD>
 static int ap_launch(const APairDev& P, bool last, hipStream_t s) {
-  using G = APairGeo<C, NPB, KS, CR, NW, V1C>;
+  using G = APairGeo<C, NPB, KS, CR, NW, V1C, WM, RD>;
   if (!g_ap_ncu) {
     int dev = 0, n = 0;
     g_ap_ncu = (hipGetDevice(&dev) == hipSuccess &&
@@ -350,28 +398,27 @@ static int ap_launch(const APairDev& P, bool last, hipStream_t s) {
   const int R8 = (P.ntiles + 7) / 8;
   int grid = 8 * std::min(g_ap_ncu * (NW == 4 ? 2 : 1) / 8, R8);
   if (knobs().ampair_grid >= 8) grid = std::min(grid, knobs().ampair_grid / 8 * 8);  // tests: several tiles per WG
-  if (last) hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, 16, true>), dim3(grid), dim3(G::NT), 0, s, P);
-  else hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, 16, false>), dim3(grid), dim3(G::NT), 0, s, P);
+  if (last)
+    hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, WM, RD, 16, true>), dim3(grid), dim3(G::NT), 0, s, P);
+  else
+    hipLaunchKernelGGL((ampair_kernel<C, NPB, KS, CR, NW, V1C, WM, RD, 16, false>), dim3(grid), dim3(G::NT), 0, s, P);
   return 0;
 }
 
-template <int C, int NPB, int CR, int NW, int V1C>
+template <int C, int NPB, int CR, int NW, int V1C, int WM, int RD>
 static int ap_by_k(const APairDev& P, int ksize, bool last, hipStream_t s) {
   switch (ksize) {
-    case 3: return ap_launch<C, NPB, 3, CR, NW, V1C>(P, last, s);
-    case 7: return ap_launch<C, NPB, 7, CR, NW, V1C>(P, last, s);
-    default: return ap_launch<C, NPB, 11, CR, NW, V1C>(P, last, s);
+    case 3: return ap_launch<C, NPB, 3, CR, NW, V1C, WM, RD>(P, last, s);
+    case 7: return ap_launch<C, NPB, 7, CR, NW, V1C, WM, RD>(P, last, s);
+    default: return ap_launch<C, NPB, 11, CR, NW, V1C, WM, RD>(P, last, s);
   }
 }
 
-// tile geometry by width (ALCM_AMPAIR_NW: 0 by shape, 4 / 8 forced where the LDS allows): C = 24 / 48 as two 4-wave
-// workgroups per CU (<= 80 KB of LDS each: one's Activation1d phases (VALU) overlap the other's convs (MFMA) and load
-// latency), 256 conv rows; C = 96 one 8-wave workgroup per CU (its operand rows alone take 64 KB)
-static int ap_waves(int C) {
-  const int nw = knobs().ampair_nw;
-  if (C == 96) return 8;
-  return nw == 8 ? 8 : 4;
-}
+// tile geometry by width (ALCM_AMPAIR_NW = 4: the first cut's two 4-wave workgroups per CU, <= 80 KB of LDS each,
+// streaming weights through a 3-slot ring).  Default, one 8-wave workgroup per CU: C = 24 keeps both convs' weights
+// resident (76 KB at k = 11) over 512 conv rows; C = 48 keeps one conv's (104 KB) and swaps it under the other phase;
+// C = 96 (its operand rows alone take 64 KB) streams through a 5-slot ring, four slices in flight
+static int ap_waves(int C) { return (C != 96 && knobs().ampair_nw == 4) ? 4 : 8; }
 static int ap_rows(int C, int nw) { return (C == 24 && nw == 8) ? 512 : 256; }
 static int ap_emitted(int C, int ksize) { return ap_rows(C, ap_waves(C)) - 12 - (ksize - 1); }
 
@@ -402,9 +449,12 @@ int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, 
   void* tok = prof_start(s);
   int rc;
   const int nw = ap_waves(C);
-  if (C == 24) rc = nw == 8 ? ap_by_k<24, 2, 512, 8, 24>(P, ksize, last, s) : ap_by_k<24, 2, 256, 4, 24>(P, ksize, last, s);
-  else if (C == 48) rc = nw == 8 ? ap_by_k<48, 2, 256, 8, 48>(P, ksize, last, s) : ap_by_k<48, 2, 256, 4, 24>(P, ksize, last, s);
-  else rc = ap_by_k<96, 1, 256, 8, 48>(P, ksize, last, s);
+  if (C == 24)
+    rc = nw == 8 ? ap_by_k<24, 2, 512, 8, 24, 1, 0>(P, ksize, last, s) : ap_by_k<24, 2, 256, 4, 24, 0, 2>(P, ksize, last, s);
+  else if (C == 48)
+    rc = nw == 8 ? ap_by_k<48, 2, 256, 8, 16, 2, 0>(P, ksize, last, s) : ap_by_k<48, 2, 256, 4, 24, 0, 2>(P, ksize, last, s);
+  else
+    rc = ap_by_k<96, 1, 256, 8, 48, 0, 4>(P, ksize, last, s);
   if (rc) return rc;
   ALCM_HIP(hipGetLastError());
   if (tok) {

@@ -601,12 +601,15 @@ def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
                                                  (96, 333, 11, 5, 2, 0), (96, 600, 7, 3, 2, 0), (24, 37, 3, 1, 3, 0),
                                                  (48, 2000, 11, 5, 3, 8), (24, 5000, 7, 1, 3, 8), (96, 1300, 11, 1, 2, 16)])
 @pytest.mark.parametrize("mode", ["state", "last"])
-def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, monkeypatch):
+@pytest.mark.parametrize("nw", [0, 4])
+def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, nw, monkeypatch):
     """One AMPBlock1 half-layer pair in one launch (alcm_ampblock_pair, vocoder/bigvgan/models.py:72-81) == the unfused
     chain it replaces: Activation1d -> operand planes, dense conv1 with the fused Activation1d epilogue, dense conv2 +
     residual (alcm_opconv_dense) — the same dense K slices, MFMA lanes and Activation1d chains, so bit-identical — incl.
     the sequence ends (replicate / zero padding), partial last tiles and several tiles per workgroup
-    (ALCM_AMPAIR_GRID); 'last' = a resblock's last pair: (x + ...) * out_scale added into the stage accumulator."""
+    (ALCM_AMPAIR_GRID); 'last' = a resblock's last pair: (x + ...) * out_scale added into the stage accumulator.
+    nw = 0: the default weight modes (C = 24 resident, C = 48 swapped, C = 96 5-slot ring); nw = 4: the 3-slot-ring
+    two-workgroups-per-CU variants (C = 24 / 48)."""
     from audiolcm_amd import _hip
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
     B = 2
@@ -623,9 +626,12 @@ def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, monkeypatch):
     else:
         ref = dev(_r((B, T, C), 139))
         K.opconv(pl2, C, w2, b2, 1, prec, residual=x, out_scale=1 / 3, accumulate_into=ref, dense=True)
-    if grid:
-        monkeypatch.setenv("ALCM_AMPAIR_GRID", str(grid))
-        _hip.reload_knobs()
+    if nw and C == 96:
+        pytest.skip("C = 96 has one geometry")
+    env = {k_: str(v) for k_, v in (("ALCM_AMPAIR_GRID", grid), ("ALCM_AMPAIR_NW", nw)) if v}
+    for k_, v in env.items():
+        monkeypatch.setenv(k_, v)
+    _hip.reload_knobs()
     try:
         if mode == "state":
             y = K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec)
@@ -633,9 +639,9 @@ def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, monkeypatch):
             y = dev(_r((B, T, C), 139))
             K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec, out_scale=1 / 3, accumulate_into=y, last=True)
     finally:
-        if grid:
-            monkeypatch.delenv("ALCM_AMPAIR_GRID")
-            _hip.reload_knobs()
+        for k_ in env:
+            monkeypatch.delenv(k_)
+        _hip.reload_knobs()
     y, ref = y.cpu(), ref.cpu()
     assert torch.isfinite(y).all()
     d = (y - ref).abs().max().item()
