@@ -65,8 +65,7 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
                     void* o_plane = nullptr);
 // whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
 bool opconv_act_supported(int prec, int N, int Cp_in);
-// actepi: const ActEpiDev* (alcm_actepi.h) or nullptr
-int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
+int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, double flops, double bytes,
               hipStream_t s);
 
 // narrow AMPBlock conv with resident dense weights (alcm_tconv.hip); actepi: const ActEpiDev* or nullptr
@@ -95,11 +94,7 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 struct Knobs {
   int wconv = 8;                 // ALCM_WCONV: > 0 = the wide-layer kernels (alcm_wconv.hip), 0 = opconv_kernel (A/B)
   int wconv_order = -1;          // ALCM_WCONV_ORDER: wconv2 workgroup order (-1 by shape, 0 M-tile major, 1 N-tile major)
-  int wconv_ablate = 0;          // ALCM_WCONV_ABLATE: timing-only ablation bits of the wide-layer kernel
-  int wconv_fpipe = 1;           // ALCM_WCONV_FPIPE: wconv2 fragment-pipelined K loop (0 = per-slice read-then-MFMA)
   int wconv3 = -1;               // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip): -1 by shape, 0 off, 1 on
-  int w3_epi = 0;                // ALCM_W3_EPI: 1 = opt-in wconv3 fp32 epilogue with 16-B accesses after an in-quad transpose (default 0: 4-B column accesses, -0.7 % end to end with 1)
-  bool text_gemm = false;        // ALCM_TEXT_GEMM: text encoders' F16 / BF16 linears on the fp32-A GEMM (A/B; default: planes)
   int wconv3_grid = 0;           // ALCM_WCONV3_GRID: cap on wconv3's persistent workgroups (tests; 0 = one per CU)
   int wconv_tile = -1;           // ALCM_WCONV_TILE: wconv2 tile, 0 = 128 x 192, 1 = 256 x 96, -1 = by shape
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width
@@ -110,7 +105,6 @@ struct Knobs {
   int act_np = 0;                // ALCM_ACT_NP: channel pairs per cooperative Activation1d tile (0 by shape, 16, 32)
   int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
   bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION
-  bool wide_act_fusion = false;  // ALCM_WIDE_ACT_FUSION
   bool no_flash = false;         // ALCM_NO_FLASH
   bool attn_tiled = false;       // ALCM_ATTN_TILED: 64-query tiled flash kernel even where K/V fit in LDS
   bool no_attn_planes = false;   // ALCM_NO_ATTN_PLANES
@@ -137,8 +131,6 @@ struct Knobs {
   int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
   int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
-  int wconv3_flat = 1;           // ALCM_WCONV3_FLAT: wconv3 on padded-flat rows for under-filled clips (0 = wconv2)
-  int wconv4 = 1;                // ALCM_WCONV4: wconv3 with the tap loop unrolled at compile time (0 = wconv3)
 };
 const Knobs& knobs();
 

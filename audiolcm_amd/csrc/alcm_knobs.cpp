@@ -18,13 +18,10 @@ static bool env_set(const char* name) {
 static Knobs read_knobs() {
   Knobs k;
   k.wconv = env_int("ALCM_WCONV", 8);
-  k.wconv_ablate = env_int("ALCM_WCONV_ABLATE", 0);
   k.wconv_order = env_int("ALCM_WCONV_ORDER", -1);
   k.wconv_tile = env_int("ALCM_WCONV_TILE", -1);
-  k.wconv_fpipe = env_int("ALCM_WCONV_FPIPE", 1);
   k.wconv3 = env_int("ALCM_WCONV3", -1);
   k.wconv3_grid = env_int("ALCM_WCONV3_GRID", 0);
-  k.w3_epi = env_int("ALCM_W3_EPI", 0);  // 16-B epilogue measured -0.7 % end to end (profiles/r3z)
   k.nconv = env_int("ALCM_NCONV", -1);
   k.nconv_nb = env_int("ALCM_NCONV_NB", 0);
   k.act_rows = env_int("ALCM_ACT_ROWS", 8) == 16 ? 16 : 8;
@@ -33,7 +30,6 @@ static Knobs read_knobs() {
   k.ups_fp32 = env_set("ALCM_UPS_FP32");
   k.opconv_tile = env_int("ALCM_OPCONV_TILE", 0);
   k.no_act_fusion = env_set("ALCM_NO_ACT_FUSION");
-  k.wide_act_fusion = env_set("ALCM_WIDE_ACT_FUSION");
   k.no_flash = env_set("ALCM_NO_FLASH");
   k.attn_tiled = env_set("ALCM_ATTN_TILED");
   k.no_attn_planes = env_set("ALCM_NO_ATTN_PLANES");
@@ -49,7 +45,6 @@ static Knobs read_knobs() {
   k.tconv_bm = env_int("ALCM_TCONV_BM", 256);
   k.tconv_stagger = env_int("ALCM_TCONV_STAGGER", -1);
   k.post_planes = env_set("ALCM_POST_PLANES");
-  k.text_gemm = env_set("ALCM_TEXT_GEMM");  // planes: 20.9 -> 13.5 ms per B = 32 text encode (profiles/r3f)
   k.sgemm = env_int("ALCM_SGEMM", 1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   k.ampair = env_int("ALCM_AMPAIR", 0);  // opt-in until it beats the unfused chain
@@ -57,8 +52,6 @@ static Knobs read_knobs() {
   k.ampair_ablate = env_int("ALCM_AMPAIR_ABLATE", 0);
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
-  k.wconv3_flat = env_int("ALCM_WCONV3_FLAT", 1);
-  k.wconv4 = env_int("ALCM_WCONV4", 0);
   return k;
 }
 

@@ -1762,7 +1762,7 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   // F16 / BF16 linears (mixed / bf16 policies) on operand planes and the plane conv kernels: the fp32-A GEMM with
   // an in-kernel conversion ran the text towers at 0.05 of the MFMA peak (profiles/r3z, bench components)
   const bool planes = (pl == PREC_F16 || pl == PREC_BF16) && H % 64 == 0 && D % 64 == 0 && TI % 64 == 0 &&
-                      X.b_inter % 64 == 0 && X.t_ff % 64 == 0 && !knobs().text_gemm;
+                      X.b_inter % 64 == 0 && X.t_ff % 64 == 0;
   for (const BertLayerW& Ly : X.bl) {
     if (planes) {
       ALCM_TRY(to_planes(w.x, w.pl, R, H, H, pl, s));

@@ -642,13 +642,9 @@ static int tile_variant(int prec) {
 bool opconv_act_supported(int prec, int N, int Cp_in) {
   if (knobs().no_act_fusion) return false;  // diagnostics / A-B
   if (N % 4 || N <= 0) return false;
-  if (N <= 96) return true;  // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%
-  // wide layers (the two-workgroup wide conv's ACT epilogue, alcm_wconv.hip): the activation's VALU work in the
-  // epilogue does not hide behind the co-resident workgroup's K loop and the 112-of-128-row tiles add 14 % MFMA
-  // work; measured -6 % end to end against conv + standalone cooperative Activation1d, so it is
-  // opt-in (ALCM_WIDE_ACT_FUSION=1) for A/B runs
-  if (!knobs().wide_act_fusion) return false;
-  return (prec == PREC_F16 || prec == PREC_BF16) && Cp_in % 64 == 0 && (N % 192 == 0 || N % 128 == 0);
+  // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%.  Wide layers keep conv + standalone
+  // Activation1d: a fused epilogue in the two-workgroup wide conv measured -6 % end to end
+  return N <= 96;
 }
 
 int opconv(const alcm_opconv_args& a, hipStream_t s) {
@@ -712,21 +708,21 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
                        M * a.N * 4.0 * ((a.out ? 1 : 0) + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0)) +
                        (act ? M * round_up(a.N, 32) * 2.0 * npa : 0.0);
   if (a.geglu_plane) {  // only the wide-layer kernel has the GEGLU epilogue
-    if (!wconv_try(a, P.w, nullptr, flops, bytes, s))
+    if (!wconv_try(a, P.w, flops, bytes, s))
       return set_error(ALCM_E_INVALID, "opconv: GEGLU plane epilogue needs F16/BF16, N % 128 == 0, Cp % 64 == 0, "
                                        "no res/accumulate/act, 4-byte aligned plane");
     ALCM_HIP(hipGetLastError());
     return 0;
   }
   if (strided) {  // the two-workgroup wide-layer kernel, or opconv_kernel's LDS-staged epilogue (N <= 96)
-    if (wconv_try(a, P.w, nullptr, flops, bytes, s)) {
+    if (wconv_try(a, P.w, flops, bytes, s)) {
       ALCM_HIP(hipGetLastError());
       return 0;
     }
     if (a.N % 4 || a.N > 96)
       return set_error(ALCM_E_INVALID, "opconv: strided output needs the wide-layer kernel (F16/BF16, N % 192 == 0, "
                                        "Cp % 64 == 0, (k-1)*dil <= 64) or N <= 96 with N % 4 == 0");
-  } else if (wconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s) ||
+  } else if ((!act && wconv_try(a, P.w, flops, bytes, s)) ||
       nconv_try(a, P.w, act ? &P.act : nullptr, flops, bytes, s)) {
     ALCM_HIP(hipGetLastError());
     return 0;

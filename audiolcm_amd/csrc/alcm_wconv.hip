@@ -2,7 +2,7 @@
 // AMPBlock convs and upsampler phases (vocoder/bigvgan/models.py:72-81, 160-165), the DiT FFN / attention projections
 // (ldm/modules/new_attention.py:48-74), the VAE k3 convs and the text encoders' wide linears.  Two kernels:
 //   * wconv2_kernel: 4 waves, two workgroups per CU (128 x 192 or 256 x 96 tiles), window staged per 64-channel
-//     chunk, weights double-buffered; strided (ConvTranspose phase), GEGLU-plane and fused-Activation1d epilogues;
+//     chunk, weights double-buffered; strided (ConvTranspose phase) and GEGLU-plane epilogues;
 //   * wconv3_kernel: one persistent 8-wave workgroup per CU walking a flat (tile, chunk, tap) step sequence.
 // Common: LDS-DMA staging (global_load_lds_dwordx4, no VGPR round trip) into lane-linear images whose 16-B slot s of
 // row r sits at s ^ (r & 7) (conflict-free ds_read_b128 fragment reads from any start row); rows outside [0, T) read
@@ -14,7 +14,7 @@
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
-#include "alcm_actepi.h"
+#include "alcm_actepi.h"  // op_store2 / f32x2 (the GEGLU plane stores)
 
 namespace alcm {
 
@@ -37,16 +37,6 @@ struct WConvDev {
   int n_major;          // workgroup order: 0 = M-tile major (N tiles of an M tile adjacent), 1 = N-tile major
   int ostride, ooff, orows;  // wconv2 output row of input row t: t * ostride + ooff of orows per batch
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
-  int tstride, tshift;  // M tile i of a batch computes rows [i * tstride - tshift, + 256)
-  ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
-  int fpipe;            // wconv2: fragment-pipelined K loop (ALCM_WCONV_FPIPE)
-  int ablate;           // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue,
-                        // 2 no MFMA, 4 no global -> LDS staging in the K loop
-  // wconv3 FLAT (padded-flat rows): the B clips laid end to end with `pad` zero rows on each side of every clip
-  // (clip b row t = flat row b * flat_tp + pad + t, flat_tp = T + 2 pad, P.T = B * flat_tp), so 256-row tiles run
-  // full across clip boundaries (VAE: T = 312 would fill 2 tiles of 256 to 61 %); gap rows read zero, are not stored
-  int flat_tlen, flat_tp;
-  FastDiv flat_div;     // / flat_tp
 };
 
 
@@ -55,12 +45,12 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Two-workgroups-per-CU variant (ALCM_WCONV=8): 4 waves, each 64 rows x 96 columns (4 x 6 16x16x32 MFMAs per
+// Two-workgroups-per-CU kernel: 4 waves, each 64 rows x 96 columns (4 x 6 16x16x32 MFMAs per
 // 32-deep K slice, 0.42 fragment reads per MFMA), tile BM x BN = 128 x 192 (waves 2 (M) x 2 (N)) or 256 x 96
 // (waves 4 (M) x 1 (N)).  <= 72 KB of LDS (one input window of BM + 64 rows x 64 channels + two weight tiles) so
 // two workgroups share a CU: the HBM-bound epilogue (fp32 output + residual + accumulate) of one overlaps the MFMA
-// K loop of the other, where the 256-row kernel above serialises them (its epilogue is 26-80 % of its time on the
-// BigVGAN shapes, scripts/microbench.py wablate).  K steps: weights double-buffered (step s+1 staged while step s
+// K loop of the other (the round-1 one-workgroup 256-row kernel serialised them: its epilogue was 26-80 % of its
+// time on the BigVGAN shapes).  K steps: weights double-buffered (step s+1 staged while step s
 // computes, vmcnt(0) + barrier per step); the window is single-buffered and re-staged at each 64-channel chunk
 // boundary (the stall is covered by the other workgroup).
 //
@@ -71,15 +61,11 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
 // halves the weight bytes (and doubles the window bytes, amortised over k taps).
 constexpr int W2_HALO = 64;  // max (k - 1) * dil
 
-// ACT (ALCM_WIDE_ACT_FUSION, 128 x 192 only): fused Activation1d epilogue (alcm_actepi.h) — tiles of 128 conv rows
-// emit the middle 112 (tstride 112, tshift 8), v = conv + bias (+ res) staged per 96-column half in LDS, fp32 out
-// for owned rows, Activation1d of owned rows written into the next conv's operand planes
-template <int PREC, bool GEGLU, int AB = 0, bool ACT = false, int BM = 128, int BN = 192>
+template <int PREC, bool GEGLU, int BM = 128, int BN = 192>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   constexpr int WGM = BM / 64, WGN = 4 / WGM;   // wave grid
   static_assert(WGM * WGN == 4 && WGN * TN * 16 == BN, "4 waves of 64 x 96");
-  static_assert(!ACT || (BM == 128 && BN == 192), "the fused activation epilogue is built for 128 x 192 tiles");
   constexpr int WROWS = BM + W2_HALO;
   constexpr int WBUF = WROWS * 128;      // window image
   constexpr int BBUF = BN * 128;         // weight image
@@ -103,7 +89,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     nt = wid - mt * P.tiles_n;
   }
   const int b = mt / P.tiles_per_batch;
-  const int t0 = (mt - b * P.tiles_per_batch) * P.tstride - P.tshift;
+  const int t0 = (mt - b * P.tiles_per_batch) * BM;
   const int col0 = nt * BN;
   const int K = P.ksize, Cp = P.Cp;
   const int WR = BM + (K - 1) * P.dil;
@@ -113,10 +99,6 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // diagnostics (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA, 4 no K-loop DMA,
-  // 8 no K-loop waits / barriers
-  constexpr bool no_dma = (AB & 4) != 0, no_mfma = (AB & 2) != 0, no_sync = (AB & 8) != 0;
-  constexpr bool no_win = (AB & 16) != 0, no_wdma = (AB & 32) != 0;  // 16: no window re-stage, 32: no weight DMA
   {
     const int nC = Cp / 64;
     const int steps = nC * K;
@@ -156,8 +138,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     stage_w(0);
     stage_b(0, 0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (P.fpipe && !no_mfma && !no_sync) {
-      // fragment-pipelined K loop (ALCM_WCONV_FPIPE, default): the second 32-deep slice's fragments are read
+    {
+      // fragment-pipelined K loop: the second 32-deep slice's fragments are read
       // while the first slice's MFMAs run (B fragments as their last use retires, A fragments after each row),
       // and the next step's A fragments (same chunk: the window is resident) during the second slice, so after
       // each step's barrier only the 6 weight-fragment reads of the new step are exposed, not 10 reads per slice
@@ -176,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       int st = 0;
       for (int c = 0; c < nC; ++c) {
         for (int tap = 0; tap < K; ++tap, ++st) {
-          if (st + 1 < steps && !no_dma) stage_b(st + 1, (st + 1) & 1);
+          if (st + 1 < steps) stage_b(st + 1, (st + 1) & 1);
           const char* Bl = smem + WBUF + (st & 1) * BBUF;
 #pragma unroll
           for (int j = 0; j < TN; ++j) bfr[j] = rdB(Bl, 0, j);
@@ -221,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
           if (tap == K - 1 && c + 1 < nC) {
             // every wave has finished reading window c: re-stage it with chunk c + 1
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (!no_dma) stage_w(c + 1);
+            stage_w(c + 1);
           }
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
           if (tap == K - 1) {
@@ -230,111 +212,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
           }
         }
       }
-    } else {
-      int st = 0;
-      for (int c = 0; c < nC; ++c) {
-        for (int tap = 0; tap < K; ++tap, ++st) {
-          if (st + 1 < steps && !no_dma && !no_wdma) stage_b(st + 1, (st + 1) & 1);
-          const char* Bl = smem + WBUF + (st & 1) * BBUF;
-          const int arow = arow0 + tap * P.dil;
-          const int asw = arow & 7;
-#pragma unroll
-          for (int sub = 0; sub < 2; ++sub) {
-            const int ls = 4 * sub + (lane >> 4);
-            bf16x8 af[TM], bfr[TN];
-            const char* ap = smem + arow * 128 + ((ls ^ asw) << 4);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ap + i * 16 * 128);
-            const char* bp = Bl + nrow0 * 128 + ((ls ^ bsw) << 4);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bp + j * 16 * 128);
-            if constexpr (no_mfma) {
-#pragma unroll
-              for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][1];
-            } else {
-              // raised priority while this wave issues its MFMA block, so the co-resident workgroup's waves (in their
-              // staging / epilogue phases) do not interleave VALU work into it (-2..-5 % on the k11 shapes)
-              __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-              for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(af[i], bfr[j], acc[i][j]);
-              __builtin_amdgcn_s_setprio(0);
-            }
-          }
-          if constexpr (no_sync) continue;
-          if (tap == K - 1 && c + 1 < nC && !no_win) {
-            // every wave has finished reading window c: re-stage it with chunk c + 1
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (!no_dma) stage_w(c + 1);
-          }
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-      }
     }
-    if constexpr (no_sync) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  }
-  if constexpr ((AB & 1) != 0) {
-    float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (sum == 123.f) P.out[tid] = sum;
-    return;
-  }
-
-  if constexpr (ACT) {
-    constexpr int HC = BN / 2;  // the 96 columns of the waves with wn == h
-    constexpr int AOTS = HC + 4;
-    constexpr int acq = HC / 4;
-    float* aot = reinterpret_cast<float*>(smem);  // 128 x 100 floats (51 KB): the K loop's last barrier retired it
-    const int e_lo = t0 + P.tshift, e_hi = min(e_lo + P.tstride, P.T);
-    for (int h = 0; h < 2; ++h) {
-      if (wn == h) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              const int nl = j * 16 + (lane & 15);
-              aot[(wm * 64 + i * 16 + (lane >> 4) * 4 + r) * AOTS + nl] =
-                  acc[i][j][r] + (P.bias ? P.bias[col0 + h * HC + nl] : 0.f);
-            }
-      }
-      __syncthreads();
-      if (P.res || P.out) {
-        for (int e = tid; e < BM * acq; e += 256) {
-          const int m = e / acq, n = (e - m * acq) * 4;
-          const int t = t0 + m;
-          if (t < 0 || t >= P.T) continue;
-          const int64_t go = ((int64_t)b * P.T + t) * P.N + col0 + h * HC + n;
-          float4 v = *reinterpret_cast<const float4*>(aot + m * AOTS + n);
-          if (P.res) {
-            const float4 rv = *reinterpret_cast<const float4*>(P.res + go);
-            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-            *reinterpret_cast<float4*>(aot + m * AOTS + n) = v;
-          }
-          if (P.out && t >= e_lo && t < e_hi) {
-            v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
-            if (P.accumulate) {
-              const float4 pv = *reinterpret_cast<const float4*>(P.out + go);
-              v.x += pv.x; v.y += pv.y; v.z += pv.z; v.w += pv.w;
-            }
-            *reinterpret_cast<float4*>(P.out + go) = v;
-          }
-        }
-        __syncthreads();
-      }
-      // 112 emitted rows: runs of 14 (8 runs x 48 channel pairs)
-      act_epilogue_tile<PREC, 14>(aot, AOTS, t0, e_lo, e_hi, P.T, HC, col0 + h * HC, P.N, b, P.act, tid, 256);
-      __syncthreads();
-    }
-    return;
   }
 
   // epilogue: one 64-row slice of the tile at a time through LDS (the K loop's last barrier retired every
@@ -443,35 +321,9 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-// v[r] of lane q of a quad = element (q, r) of a 4 x 4 block -> element (r, q): two DPP butterflies (xor 1, xor 2)
-__device__ __forceinline__ float w3_dpp_xor(float x, int ctrl_is_xor2) {
-  const int i = __builtin_bit_cast(int, x);
-  return __builtin_bit_cast(float, ctrl_is_xor2 ? __builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, true)
-                                                : __builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, true));
-}
-__device__ __forceinline__ void w3_quad_transpose(float (&v)[4], int q) {
-#pragma unroll
-  for (int p = 0; p < 4; p += 2) {
-    const float t = w3_dpp_xor((q & 1) ? v[p] : v[p + 1], 0);
-    if (q & 1) v[p] = t; else v[p + 1] = t;
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float t = w3_dpp_xor((q & 2) ? v[p] : v[p + 2], 1);
-    if (q & 2) v[p] = t; else v[p + 2] = t;
-  }
-}
-
-// AB (ALCM_WCONV_ABLATE, timing only, results wrong): 1 no epilogue, 4 no K-loop DMA, 16 no K-loop waits /
-// barriers.  GEGLU: the DiT FFN
-// up-projection's epilogue (new_attention.py:48-55): interleaved columns (2m, 2m+1) = (value m, gate m) ->
-// value * gelu_erf(gate) into the operand plane P.gplane [B][T][N/2].  EPI4: the fp32 epilogue with 16-B
-// accesses after an in-quad transpose (ALCM_W3_EPI=0: the 4-B column-access epilogue, A/B)
-template <int PREC, int AB, bool GEGLU = false, bool EPI4 = true, bool FLAT = false>
+template <int PREC>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
-  static_assert(!FLAT || (!GEGLU && !EPI4), "padded-flat rows: the 4-B fp32 epilogue");
   constexpr int TM = 4, TN = 6;
-  constexpr bool ab_dma = (AB & 4) != 0, ab_sync = (AB & 16) != 0;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -518,14 +370,8 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   auto win_piece = [&](int j) {
     const int row = 8 * (wave + 8 * j) + (lane >> 3);
     const int ls = (lane & 7) ^ (row & 7);
-    int ts = wrow0 + row;
-    bool ok = row < WR && ts >= 0 && ts < P.T;
-    if constexpr (FLAT) {  // padded-flat row -> (clip, row of the clip); the gap rows are zero
-      const int bq = (int)P.flat_div.div((uint32_t)max(ts, 0));
-      const int tt = ts - bq * P.flat_tp - P.pad;
-      ok = ok && tt >= 0 && tt < P.flat_tlen;
-      ts = bq * P.flat_tlen + tt;
-    }
+    const int ts = wrow0 + row;
+    const bool ok = row < WR && ts >= 0 && ts < P.T;
     const u16* src = ok ? wsrc_base + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
     glds16(src, smem + wbuf * W3_WBUF + (wave + 8 * j) * 1024);
   };
@@ -537,8 +383,9 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   // the next chunk's window is spread over the current chunk's first K - 2 steps (piece j at tap j % (K - 2)), so
   // the whole grid's window stream (40 KB per CU per chunk) does not land as one burst that queues the weight DMA
   // behind it (a burst every 11 steps cost 12 % in scripts/probes/mfma_lds_probe.hip); issued no later than tap
-  // K - 3, every piece is covered by the counted wait at the chunk's last mid-step
-  const int wspread = P.fpipe ? 1 : K - 2;  // ALCM_WCONV3=2 (A/B): the whole window at the chunk's first step
+  // K - 3, every piece is covered by the counted wait at the chunk's last mid-step (a burst at the chunk's first
+  // step measured equal within 2 %)
+  const int wspread = K - 2;
 
   // weight DMA: per-lane 32-bit byte offsets (row n * kpad + 16-B piece) from a workgroup-uniform base, so each
   // instruction is a saddr + voffset access with no per-step 64-bit address arithmetic; instruction j covers rows
@@ -642,21 +489,18 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     //      issued after weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay
     //      in flight
     const bool chunk_end = tap == K - 1;
-    if constexpr (ab_sync) {
-    } else switch (pieces_last) {
+    switch (pieces_last) {
       case 0: w3_wait_barrier<W3_BPW>(); break;
       case 1: w3_wait_barrier<W3_BPW + 1>(); break;
       case 2: w3_wait_barrier<W3_BPW + 2>(); break;
       default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
     }
     pieces_last = 0;
-    if constexpr (!ab_dma) {
-      if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
-        if (tap == 0) win_setup(q + 1);
-        for (int j = tap; j < W3_WPW; j += wspread) {
-          win_piece(j);
-          ++pieces_last;
-        }
+    if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
+      if (tap == 0) win_setup(q + 1);
+      for (int j = tap; j < W3_WPW; j += wspread) {
+        win_piece(j);
+        ++pieces_last;
       }
     }
 
@@ -676,15 +520,15 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
         // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
-        if constexpr (!ab_dma) issue_wt(sl);
+        issue_wt(sl);
       }
     }
     __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
-    if constexpr (!ab_dma) __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
+    __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
     __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (!ab_dma) advance_wt();
+    advance_wt();
 
     sl = sl1;
     if (!chunk_end) {
@@ -695,62 +539,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     ++q;
     if (++c == nC) {
       // ---- tile epilogue, straight from the accumulators (fp32 out = (acc + bias + res) * scale (+ out))
-      if constexpr ((AB & 1) == 0 && GEGLU) {
-        int b, t0, col0;
-        tile_of(ti, b, t0, col0);
-        float bv[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
-        // every lane evaluates gelu of its own column (one instruction stream for all lanes); the value lane of a
-        // pair takes the gate's from its neighbour, and lane 4q stores the two outputs of columns 4q .. 4q + 3
-        const int No = P.N / 2;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-            u16* orow = P.gplane + ((int64_t)b * P.T + min(t, P.T - 1)) * No + (col0 + wn * 96 + (lane & 15)) / 2;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              const float x = acc[i][j][r] + bv[j];
-              const float gx = alcm_act(x, ACT_GELU_ERF);
-              const float y = x * __shfl_xor(gx, 1);
-              const float y2 = __shfl_xor(y, 2);
-              if ((lane & 3) == 0 && t < P.T) op_store2<PREC>(orow + j * 8, 0, f32x2{y, y2});
-            }
-          }
-      } else if constexpr ((AB & 1) == 0 && EPI4) {
-        // 4 x 4 transpose inside each lane quad (two DPP butterfly stages): lane q of a quad then owns ROW
-        // 4 (lane >> 4) + q of the fragment at columns (lane & 12) .. + 3, so bias / residual / accumulate / out move
-        // as one 16-B access per lane per fragment instead of four 4-B column accesses (12 -> 3 memory instructions)
-        int b, t0, col0;
-        tile_of(ti, b, t0, col0);
-        const int q = lane & 3;
-        const int cb = col0 + wn * 96 + (lane & 12);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + q;
-          const int64_t ro = ((int64_t)b * P.T + min(t, P.T - 1)) * P.N + cb;
-          float4 rv[TN], pv[TN];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            rv[j] = P.res ? *reinterpret_cast<const float4*>(P.res + ro + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-            pv[j] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + ro + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            w3_quad_transpose(v, q);
-            const float4 bv = P.bias ? *reinterpret_cast<const float4*>(P.bias + cb + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 o;
-            o.x = (v[0] + bv.x + rv[j].x) * P.out_scale + pv[j].x;
-            o.y = (v[1] + bv.y + rv[j].y) * P.out_scale + pv[j].y;
-            o.z = (v[2] + bv.z + rv[j].z) * P.out_scale + pv[j].z;
-            o.w = (v[3] + bv.w + rv[j].w) * P.out_scale + pv[j].w;
-            if (t < P.T) *reinterpret_cast<float4*>(P.out + ro + j * 16) = o;
-          }
-        }
-      } else if constexpr ((AB & 1) == 0) {
+      {
         int b, t0, col0;
         tile_of(ti, b, t0, col0);
         float bv[TN];
@@ -763,13 +552,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-            if constexpr (FLAT) {
-              const int bq = (int)P.flat_div.div((uint32_t)t);
-              const int tt = t - bq * P.flat_tp - P.pad;
-              orow[r] = (t < P.T && tt >= 0 && tt < P.flat_tlen) ? bq * P.flat_tlen + tt : -1;
-            } else {
-              orow[r] = t < P.T ? b * P.T + t : -1;
-            }
+            orow[r] = t < P.T ? b * P.T + t : -1;
             const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -786,13 +569,6 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
               P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
           }
         }
-      } else {
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (sum == 123.f) P.out[tid] = sum;
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -804,254 +580,14 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// wconv4: wconv3's tile, LDS images, fragment pipeline and epilogue with the tap loop unrolled at compile time
-// (KS = 3 / 5 / 7 / 9 / 11).  Per step, everything wconv3 decides at run time is then a constant of the unrolled
-// code: whether the step ends a chunk, which window pieces it issues and so the counted vmcnt of its mid-step wait,
-// the next step's tap, and whether the weight step it issues 3 ahead lies in this chunk or the next one (two bases
-// per chunk instead of the per-step cursor with its chunk / tile switches).  Chunk and tile bookkeeping runs once
-// per chunk.  Past the last step the kernel re-issues valid addresses (the loads land in buffers nobody reads) so the
-// counted waits stay exact.  Bit-identical to wconv3 (same products in the same order).
-template <int I, int N, class F>
-__device__ __forceinline__ void w4_static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    w4_static_for<I + 1, N>(f);
-  }
-}
-
-template <int PREC, int KS, bool FLAT>
-__global__ __launch_bounds__(512, 1) void wconv4_kernel(const WConvDev P) {
-  constexpr int TM = 4, TN = 6;
-  static_assert(KS >= 3, "three weight steps in flight");
-  constexpr int WSP = KS - 2;  // window pieces of the next chunk spread over taps < min(WSP, W3_WPW)
-  __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
-  const int ntiles = P.nwg;
-  const int R8 = (ntiles + 7) >> 3;
-  const int tbeg = xcd * R8, tend = min(tbeg + R8, ntiles);
-  const int first = tbeg + slot;
-  const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
-  if (my_n == 0) return;
-  const int Cp = P.Cp, nC = Cp / 64, dil = P.dil;
-  const int WR = W3_BM + (KS - 1) * dil;
-  const int tiles_m = ntiles / P.tiles_n;
-  auto tile_of = [&](int ti, int& b, int& t0, int& col0) {
-    const int tile = first + min(ti, my_n - 1) * nslot;  // (clamped: past the last tile, re-point at it)
-    int mt, nt;
-    if (P.n_major) {
-      nt = tile / tiles_m;
-      mt = tile - nt * tiles_m;
-    } else {
-      mt = tile / P.tiles_n;
-      nt = tile - mt * P.tiles_n;
-    }
-    b = mt / P.tiles_per_batch;
-    t0 = (mt - b * P.tiles_per_batch) * W3_BM;
-    col0 = nt * W3_BN;
-  };
-  // window of chunk (ti, c) -> buffer wb: W3_WPW DMA instructions of 8 rows x 128 B per wave
-  const u16* wsrc = P.a;
-  int wrow0 = 0;
-  auto win_setup = [&](int ti, int c) {
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
-    wsrc = P.a + (int64_t)b * P.T * Cp + c * 64;
-    wrow0 = t0 - P.pad;
-  };
-  auto win_piece = [&](int j, int wb) {
-    const int row = 8 * (wave + 8 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (row & 7);
-    int ts = wrow0 + row;
-    bool ok = row < WR && ts >= 0 && ts < P.T;
-    if constexpr (FLAT) {
-      const int bq = (int)P.flat_div.div((uint32_t)max(ts, 0));
-      const int tt = ts - bq * P.flat_tp - P.pad;
-      ok = ok && tt >= 0 && tt < P.flat_tlen;
-      ts = bq * P.flat_tlen + tt;
-    }
-    const u16* src = ok ? wsrc + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
-    glds16(src, smem + wb * W3_WBUF + (wave + 8 * j) * 1024);
-  };
-  uint32_t boff[W3_BPW];
-#pragma unroll
-  for (int j = 0; j < W3_BPW; ++j) {
-    const int n = 8 * (wave + 8 * j) + (lane >> 3);
-    boff[j] = (uint32_t)(n * P.kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
-  }
-  auto issue_wt = [&](int64_t off, int sl) {  // weight step at element offset `off` -> ring slot sl
-    const char* base = reinterpret_cast<const char*>(P.w + off);
-#pragma unroll
-    for (int j = 0; j < W3_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 8 * j) * 1024);
-  };
-  auto wbase = [&](int ti, int c) -> int64_t {  // weight element offset of (tile ti, chunk c, tap 0)
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
-    return (int64_t)col0 * P.kpad + c * 64;
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int arow0 = wm * 64 + (lane & 15);
-  const int nrow0 = wn * 96 + (lane & 15);
-  const int bsw = lane & 7;
-  auto rdA = [&](int buf, int tp, int sub, int i) -> bf16x8 {
-    int arow = arow0 + tp * dil;
-    asm volatile("" : "+v"(arow));  // recomputed per read: hoisting KS per-tap addresses out of the chunk loop spills
-    return *reinterpret_cast<const bf16x8*>(smem + buf * W3_WBUF + arow * 128 +
-                                            (((4 * sub + (lane >> 4)) ^ (arow & 7)) << 4) + i * 16 * 128);
-  };
-  auto rdB = [&](int sl, int sub, int j) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(smem + 2 * W3_WBUF + sl * W3_BBUF + nrow0 * 128 +
-                                            (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
-  };
-
-  // prologue: window (0, 0); weight steps 0, 1, 2 (all in chunk 0: KS >= 3)
-  int64_t wb_cur = wbase(0, 0);
-  win_setup(0, 0);
-#pragma unroll
-  for (int j = 0; j < W3_WPW; ++j) win_piece(j, 0);
-  issue_wt(wb_cur, 0);
-  issue_wt(wb_cur + Cp, 1);
-  issue_wt(wb_cur + 2 * Cp, 2);
-  w3_wait_barrier<2 * W3_BPW>();
-  bf16x8 aA[TM], aB[TM], bA[TN], bB[TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) aA[i] = rdA(0, 0, 0, i);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
-
-  int sl = 0;   // ring slot of the current step
-  int q = 0;    // global chunk: window buffer q & 1
-  for (int ti = 0; ti < my_n; ++ti) {
-    for (int c = 0; c < nC; ++c, ++q) {
-      // the chunk after this one (the next tile's first, or past the end: this one again)
-      const bool last_c = c + 1 == nC;
-      const int nti = last_c ? ti + 1 : ti, nc = last_c ? 0 : c + 1;
-      const int64_t wb_next = (nti < my_n) ? wbase(nti, nc) : wb_cur;
-      const int wbuf = q & 1;
-      w4_static_for<0, KS>([&](auto tap_c) {
-        constexpr int tap = decltype(tap_c)::value;
-        // ---- slice 0 on (aA, bA); slice 1's fragments read under it
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
-          if (i == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
-#pragma unroll
-            for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(wbuf, tap, 1, ii);
-          }
-        }
-        __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
-        __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-        __builtin_amdgcn_s_setprio(0);
-        // ---- mid-step: weight step g + 1 resident (and, at the chunk's last tap, the next chunk's window: its
-        //      pieces went out at taps <= KS - 3, before weight step g + 1); what the previous mid-step issued and
-        //      weight step g + 2 stay in flight
-        constexpr int prev = tap == 0 ? 0 : (tap - 1 < WSP && tap - 1 < W3_WPW ? (W3_WPW - (tap - 1) + WSP - 1) / WSP : 0);
-        w3_wait_barrier<W3_BPW + prev>();
-        if constexpr (tap < WSP && tap < W3_WPW) {
-          if constexpr (tap == 0) {
-            if (nti < my_n) win_setup(nti, nc);  // (no next chunk: re-stage this one into the idle buffer)
-          }
-#pragma unroll
-          for (int j = tap; j < W3_WPW; j += WSP) win_piece(j, wbuf ^ 1);
-        }
-        // ---- slice 1 on (aB, bB); the next step's slice-0 fragments read under it; weight step g + 3 issued into
-        //      the slot this step has finished reading
-        const int sl1 = sl == 2 ? 0 : sl + 1;
-        constexpr bool cend = tap == KS - 1;
-        const int nbuf = cend ? wbuf ^ 1 : wbuf;
-        constexpr int ntap = cend ? 0 : tap + 1;
-        const int64_t woff = (tap + 3 < KS) ? wb_cur + (tap + 3) * Cp : wb_next + (tap + 3 - KS) * Cp;
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
-          if (i == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
-#pragma unroll
-            for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
-            issue_wt(woff, sl);
-          }
-        }
-        __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
-        __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
-        __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-        __builtin_amdgcn_s_setprio(0);
-        sl = sl1;
-        __builtin_amdgcn_sched_barrier(0);  // no code motion across steps (live ranges of the unrolled taps)
-      });
-      wb_cur = wb_next;
-    }
-    // ---- tile epilogue from the accumulators: out = (acc + bias + res) * scale (+ out)
-    {
-      int b, t0, col0;
-      tile_of(ti, b, t0, col0);
-      float bv[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float rv[4][TN], pv[4][TN];
-        int orow[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-          if constexpr (FLAT) {
-            const int bq = (int)P.flat_div.div((uint32_t)t);
-            const int tt = t - bq * P.flat_tp - P.pad;
-            orow[r] = (t < P.T && tt >= 0 && tt < P.flat_tlen) ? bq * P.flat_tlen + tt : -1;
-          } else {
-            orow[r] = t < P.T ? b * P.T + t : -1;
-          }
-          const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
-            pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (orow[r] < 0) continue;
-          const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
 static int g_ncu = 0;
 
 // Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
-// residual, scale, accumulate; no GEGLU / strided / fused activation).  Returns 1 when it launched.
-static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s,
-                      bool flat) {
+// residual, scale, accumulate; no GEGLU / strided output).  Returns 1 when it launched.
+static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  const bool gl = a.geglu_plane != nullptr;
-  if (a.out_act || a.out_stride > 0 || a.Cp % 64 || a.ksize < 3 || (a.ksize - 1) * a.dil > 64 || a.N % W3_BN ||
-      (!gl && !a.out) || (gl && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))))
+  if (a.out_act || a.out_stride > 0 || a.geglu_plane || !a.out || a.Cp % 64 || a.ksize < 3 ||
+      (a.ksize - 1) * a.dil > 64 || a.N % W3_BN)
     return 0;
   if (!g_ncu) {
     int dev = 0, n = 0;
@@ -1066,20 +602,9 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
-  P.gplane = (u16*)a.geglu_plane;
-  P.fpipe = knobs().wconv3 == 2;  // wconv3: window DMA in one burst instead of spread over the chunk's steps
-  int nb = a.B;
-  if (flat) {
-    P.flat_tlen = a.T;
-    P.flat_tp = a.T + 2 * a.pad;
-    P.flat_div = FastDiv((uint32_t)P.flat_tp);
-    if ((int64_t)a.B * P.flat_tp >= (1ll << 31)) return 0;
-    P.T = a.B * P.flat_tp;
-    nb = 1;
-  }
   P.tiles_per_batch = (P.T + W3_BM - 1) / W3_BM;
   P.tiles_n = a.N / W3_BN;
-  const int64_t nt = (int64_t)nb * P.tiles_per_batch * P.tiles_n;
+  const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
   if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
   if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
   P.nwg = (int)nt;
@@ -1089,56 +614,11 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  const int ab = knobs().wconv_ablate;
-  const bool e4req = knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15);
-  const int ks = a.ksize;
-  const bool w4 = knobs().wconv4 && !gl && !ab && (flat || !e4req) && (ks == 3 || ks == 5 || ks == 7 || ks == 9 || ks == 11);
-  if (w4) {
-    auto go4 = [&](auto kc, auto fc) {
-      constexpr int KSC = decltype(kc)::value;
-      constexpr bool FL = decltype(fc)::value;
-      if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv4_kernel<PREC_F16, KSC, FL>), dim3(grid), dim3(512), 0, s, P);
-      else hipLaunchKernelGGL((wconv4_kernel<PREC_BF16, KSC, FL>), dim3(grid), dim3(512), 0, s, P);
-    };
-    auto byk = [&](auto fc) {
-      switch (ks) {
-        case 3: go4(std::integral_constant<int, 3>{}, fc); break;
-        case 5: go4(std::integral_constant<int, 5>{}, fc); break;
-        case 7: go4(std::integral_constant<int, 7>{}, fc); break;
-        case 9: go4(std::integral_constant<int, 9>{}, fc); break;
-        default: go4(std::integral_constant<int, 11>{}, fc); break;
-      }
-    };
-    if (flat) byk(std::true_type{});
-    else byk(std::false_type{});
-  } else if (ab && a.prec == PREC_F16) {
-    switch (ab) {
-#define W3AB(v) case v: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, v>), dim3(grid), dim3(512), 0, s, P); break;
-      W3AB(1) W3AB(4) W3AB(5) W3AB(21)
-#undef W3AB
-      default: hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P); break;
-    }
-  } else if (gl) {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, true>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, true>), dim3(grid), dim3(512), 0, s, P);
-  } else if (flat) {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, false, false, true>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, false, false, true>), dim3(grid), dim3(512), 0, s, P);
-  } else if (knobs().w3_epi && !(((uintptr_t)a.out | (uintptr_t)a.res | (uintptr_t)a.bias) & 15)) {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0>), dim3(grid), dim3(512), 0, s, P);
-  } else {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 0, false, false>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 0, false, false>), dim3(grid), dim3(512), 0, s, P);
-  }
+  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
-    const bool e4 = !flat && (gl || e4req);
-    if (w4)
-      std::snprintf(name, sizeof(name), "alcm::wconv4_kernel<%d, %d, %s>", a.prec, ks, flat ? "true" : "false");
-    else
-      std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 0, %s, %s%s>", a.prec, gl ? "true" : "false",
-                    e4 ? "true" : "false", flat ? ", true" : "");
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -1149,7 +629,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
 
 // wconv2 tile by shape (ALCM_WCONV_TILE = -1): 256 x 96 where the weight stream dominates the per-CU fetch (k >= 7:
 // the window is amortised over >= 7 taps) and there is at least one 256-row tile per CU; 128 x 192 elsewhere.
-// Measured per launch (B = 32, scripts/microbench.py wablate, one box): s0 C768 k11 0.946 -> 0.860 ms, s1 C384 k11
+// Measured per launch (B = 32, one box): s0 C768 k11 0.946 -> 0.860 ms, s1 C384 k11
 // 0.973 -> 0.934, s2 C192 k11 0.583 -> 0.559, DiT FFN-down 0.377 -> 0.358; k3 shapes equal or slower (VAE k3 +17 %)
 static bool wconv2_tile256(const alcm_opconv_args& a) {
   const int64_t mt = (int64_t)a.B * ((a.T + 255) / 256);
@@ -1158,41 +638,33 @@ static bool wconv2_tile256(const alcm_opconv_args& a) {
 
 // Eligible: single-plane precisions, N a multiple of 192 (128 x 192 tiles) or 96 (256 x 96 tiles), Cp a multiple of
 // 64, (k-1)d <= 64, no output activation.  Returns 1 when it launched, 0 when the caller should use opconv_kernel
-// (ALCM_WCONV=0: always 0 for plain same-length convs, the A/B reference; strided / GEGLU / fused-activation
-// epilogues exist only here).
-int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, double flops, double bytes,
-              hipStream_t s) {
+// (ALCM_WCONV=0: always 0 for plain same-length convs, the A/B reference; the strided and GEGLU epilogues exist
+// only here).
+int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
   const bool off = knobs().wconv <= 0;
   const bool strided = a.out_stride > 0;
-  const bool act = actepi != nullptr;
   // persistent 8-wave kernel (ALCM_WCONV3: -1 by shape, 0 off, 1 wherever eligible): by shape where the 256-row
-  // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %),
-  // not for the GEGLU up-projection (its register epilogue evaluates erf on every lane: 5.25 vs 4.94 ms/step)
+  // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %,
+  // nor with the clips laid end to end as padded-flat rows: 2.85 vs 2.61 ms/step on wconv2)
   const int w3 = knobs().wconv3;
   const int mt256 = (a.T + W3_BM - 1) / W3_BM;
   const bool full = a.T * 100 >= mt256 * W3_BM * 85;
-  // padded-flat rows (ALCM_WCONV3_FLAT, default on) where the per-clip 256-row tiles would be under 85 % full but the
-  // clips laid end to end fill them (the VAE's T = 312 / 624 k3 convs: 61 / 81 % -> 98 / 99 %)
-  const int64_t fr = (int64_t)a.B * (a.T + 2 * a.pad);
-  const bool flat = !full && !a.geglu_plane && a.B > 1 && knobs().wconv3_flat &&
-                    (int64_t)a.B * a.T * 100 >= (fr + W3_BM - 1) / W3_BM * W3_BM * 85;
-  if (!off && w3 != 0 && !act && !strided && (w3 > 0 || ((full || flat) && !a.geglu_plane)) &&
-      wconv3_try(a, wplane, flops, bytes, s, flat && !(w3 > 0 && full)))
+  if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || full) && wconv3_try(a, wplane, flops, bytes, s))
     return 1;
-  if (off && !act && !a.geglu_plane && !strided) return 0;
+  if (off && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > W2_HALO) return 0;
   if (a.N % 96) return 0;
-  if (!act && !a.geglu_plane && !strided && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
+  if (!a.geglu_plane && !strided && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
                                                                                      // 128-row tiles fill the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
-  if (a.geglu_plane && (act || a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
+  if (a.geglu_plane && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
   // wconv2 tile (ALCM_WCONV_TILE): 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
   const int tk = knobs().wconv_tile;
-  const bool t256 = !act && a.N % 96 == 0 && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
+  const bool t256 = a.N % 96 == 0 && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
   const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
-  if (!(act && strided) && a.N % BN2 == 0) {
+  if (a.N % BN2 == 0) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
@@ -1202,21 +674,15 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     P.ostride = strided ? a.out_stride : 1;
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;
-    P.ablate = act ? 0 : knobs().wconv_ablate;
-    P.fpipe = knobs().wconv_fpipe;
-    // ACT tiles overlap by 2 * ACT_EPI_HALO rows: each computes 128 conv rows and emits the middle 112
-    P.tstride = act ? BM2 - 2 * ACT_EPI_HALO : BM2;
-    P.tshift = act ? ACT_EPI_HALO : 0;
-    if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
     // N-tile-major order where the weight matrix is long (Cp * k >= 4096) and there are enough M tiles to share
     // an XCD's weight slice: that XCD's N tiles stay in its L2 (C768 k11 -17 %, DiT FFN -3..-10 %); M-major
     // elsewhere (the N tiles of an M tile share its input window in L2)
-    const int tiles_m = a.B * ((a.T + P.tstride - 1) / P.tstride);
+    const int tiles_m = a.B * ((a.T + BM2 - 1) / BM2);
     const int ord = knobs().wconv_order;
     // (the GEGLU up-projection, 64 M tiles x 48 N tiles of 1 MB weight slices: N-major -4 %, its M-major order
     // re-reads the weights from the Infinity Cache once per M tile, 3 GB counted per launch)
     P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && (tiles_m >= 128 || (a.geglu_plane && tiles_m >= 64)));
-    P.tiles_per_batch = (a.T + P.tstride - 1) / P.tstride;
+    P.tiles_per_batch = (a.T + BM2 - 1) / BM2;
     P.tiles_n = a.N / BN2;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
     if (nwg2 >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
@@ -1226,25 +692,15 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     const bool gl = a.geglu_plane != nullptr;
     auto go = [&](auto bm_c) {
       constexpr int BM = decltype(bm_c)::value, BN = BM == 256 ? 96 : 192;
-      if (a.prec == PREC_F16 && !gl && P.ablate) {
-        switch (P.ablate) {
-          case 1: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 1, false, BM, BN>), grid, blk, 0, s, P); break;
-          case 2: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 2, false, BM, BN>), grid, blk, 0, s, P); break;
-          case 4: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 4, false, BM, BN>), grid, blk, 0, s, P); break;
-          default: hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 5, false, BM, BN>), grid, blk, 0, s, P); break;
-        }
-      } else if (a.prec == PREC_F16) {
-        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true, 0, false, BM, BN>), grid, blk, 0, s, P);
-        else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 0, false, BM, BN>), grid, blk, 0, s, P);
+      if (a.prec == PREC_F16) {
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, BM, BN>), grid, blk, 0, s, P);
       } else {
-        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true, 0, false, BM, BN>), grid, blk, 0, s, P);
-        else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, 0, false, BM, BN>), grid, blk, 0, s, P);
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, BM, BN>), grid, blk, 0, s, P);
       }
     };
-    if (act) {
-      if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, 0, true>), grid, blk, 0, s, P);
-      else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, 0, true>), grid, blk, 0, s, P);
-    } else if (t256) {
+    if (t256) {
       go(std::integral_constant<int, 256>{});
     } else {
       go(std::integral_constant<int, 128>{});
@@ -1252,8 +708,8 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     if (tok) {
       char name[112];
       // the demangled rocprofv3 name (template defaults included), so bench.py can join the PMC passes by name
-      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s, 0, %s, %d, %d>", a.prec, gl ? "true" : "false",
-                    act ? "true" : "false", BM2, BN2);
+      std::snprintf(name, sizeof(name), "alcm::wconv2_kernel<%d, %s, %d, %d>", a.prec, gl ? "true" : "false", BM2,
+                    BN2);
       if (knobs().prof_shapes)
         std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp,
                       a.N, a.ksize);

@@ -162,51 +162,6 @@ WIDE_SHAPES = [  # (name, T, Cin, N, k, dil, geglu, residual, accumulate) at B =
     ("vae k3", 312, 1536, 1536, 3, 1, False, True, False)]
 
 
-def bench_wablate(B=32):
-    """wide-layer kernel phase costs (ALCM_WCONV_ABLATE bits: 1 no epilogue, 2 no MFMA, 4 no K-loop staging;
-    timing only) on every shape the bench runs it on"""
-    sel = os.environ.get("WSHAPES")
-    for name, T, Cin, N, k, d, gl, res, acc in WIDE_SHAPES:
-        if sel and not any(x in name for x in sel.split(",")):
-            continue
-        x = torch.randn((B, T, Cin), device="cuda")
-        w = torch.randn((N, Cin, k), device="cuda") / (Cin * k) ** 0.5
-        b = torch.randn(N, device="cuda") * 0.05
-        r = torch.randn((B, T, N), device="cuda") if res else None
-        o = torch.zeros((B, T, N), device="cuda") if acc else None
-        pw = K.pack_conv_weight(w)
-        pl = K.operand_planes(x, 2)
-        tf = 2 * B * T * Cin * N * k / 1e12
-        line, outs = [], []
-        # variants: KNOBS="ALCM_WCONV_TILE=0+ALCM_WCONV_FPIPE=0,ALCM_WCONV_TILE=1" (one ALCM_* assignment set each)
-        for var in os.environ.get("KNOBS", "ALCM_WCONV=8").split(","):
-            kv = dict(x.split("=") for x in var.split("+"))
-            os.environ.update(kv)
-            for ab in os.environ.get("ABLATE", "0,1,2,4,6,3").split(","):
-                os.environ["ALCM_WCONV_ABLATE"] = ab
-                _hip.reload_knobs()
-                if gl:
-                    fn = lambda: K.opconv(pl, Cin, w, b, d, 2, packed=pw, geglu=True)
-                else:
-                    fn = lambda: K.opconv(pl, Cin, w, b, d, 2, residual=r, packed=pw, accumulate_into=o)
-                ms = timeit(fn, reps=5)
-                if ab == "0":
-                    if o is not None:
-                        o.zero_()
-                    y = fn()
-                    yy = y if y is not None else o
-                    outs.append((yy.view(torch.float16) if yy.dtype == torch.int16 else yy).float().clone())
-                line.append(f"{'/'.join(v for v in kv.values())}ab{ab} {ms:7.3f}")
-            for k in kv:
-                os.environ.pop(k)
-        os.environ.pop("ALCM_WCONV_ABLATE")
-        _hip.reload_knobs()
-        ms0 = float(line[0].split()[1])
-        diff = max([float((outs[0] - x).abs().max()) for x in outs[1:]] or [0.0])
-        print(f"{name:12s} {tf / ms0 * 1e3:7.1f} TF/s | " + " | ".join(line) + f" ms | max|diff| {diff:.2e}",
-              flush=True)
-
-
 def bench_wone(B=32):
     """the WSHAPES wide-layer shapes, 5 launches each with the current ALCM_* settings (target of --pmc passes)"""
     sel = os.environ.get("WSHAPES", "s0 C768 k11")
@@ -469,4 +424,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wablate": bench_wablate, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
