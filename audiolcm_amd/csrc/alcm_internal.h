@@ -117,7 +117,7 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
-  int sgemm = 1;                 // ALCM_SGEMM: DiT proj_in / proj_out on split planes (alcm_sgemm.hip), 0 = gemm_kernel
+  int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip; 1 / 2 / 3 = kernel variant), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
   bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)
   int tconv_stagger = -1;        // ALCM_TCONV_STAGGER: streamed narrow conv grid: -1 by shape, 0 one workgroup per tile, >= 1 persistent (stagger - 1 sleeps)

@@ -45,15 +45,25 @@ __device__ __forceinline__ void sg_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
 }
 
-constexpr int SG_STAGES = 3;  // K stages in flight: the DiT shapes give ~1.4 workgroups per CU, so latency hides
-                              // in the ring, not behind a second workgroup
-
-__global__ __launch_bounds__(256, 1) void sgemm_planes_kernel(const SGemmDev P) {
+// Variants (ALCM_SGEMM: 1 = KD 32, 3 stages, one workgroup per CU; 2 = KD 64 (whole 128-B row segments per DMA
+// lane group), 2 stages, one per CU; 3 = KD 32, 2 stages, two workgroups per CU).  KD-deep K stages of both planes of
+// both operands are DMA'd NST - 1 stages ahead into an NST-stage ring; rows of KD * 2 bytes, the 16-B chunk kq of row r
+// at slot kq ^ (r & 7) (KD 64) / kq ^ ((r >> 2) & 2) (KD 32): conflict-free ds_read_b128
+template <int KD, int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P) {
   constexpr int TM = 4, TN = 6;
-  constexpr int AB = SG_BM * 64;          // one plane of the A stage (8 KB)
-  constexpr int BB = SG_BN * 64;          // one plane of the B stage (12 KB)
-  constexpr int STAGE = 2 * AB + 2 * BB;  // 40 KB
-  __shared__ __attribute__((aligned(1024))) char smem[SG_STAGES * STAGE];
+  constexpr int RB = KD * 2;              // LDS row bytes
+  constexpr int AB = SG_BM * RB;          // one plane of the A stage
+  constexpr int BB = SG_BN * RB;          // one plane of the B stage
+  constexpr int STAGE = 2 * AB + 2 * BB;  // 40 / 80 KB
+  constexpr int RPI = 1024 / RB;          // rows per DMA instruction (16 / 8)
+  constexpr int LPR = RB / 16;            // lanes per row (4 / 8)
+  constexpr int AIW = SG_BM / RPI / 4;    // A instructions per plane per wave (2 / 4)
+  constexpr int BIW = SG_BN / RPI / 4;    // B instructions per plane per wave (3 / 6)
+  constexpr int DPW = 2 * (AIW + BIW);    // DMA instructions per wave per stage (10 / 20)
+  constexpr int SUB = KD / 32;            // 32-deep MFMA slices per stage
+  static_assert(NST * STAGE <= 163840 / OCC, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware order: consecutive work ids (the N tiles of one M tile: they share the A rows) on one XCD
@@ -62,33 +72,32 @@ __global__ __launch_bounds__(256, 1) void sgemm_planes_kernel(const SGemmDev P) 
   const int wid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
   const int mt = wid / P.tiles_n, nt = wid - mt * P.tiles_n;
   const int m0 = mt * SG_BM, n0 = nt * SG_BN;
+  auto swz = [](int kq, int r) { return KD == 64 ? kq ^ (r & 7) : kq ^ ((r >> 2) & 2); };
 
-  // DMA sources: instruction i of a plane covers 16 rows x 64 B; lane -> (row i*16 + lane/4, physical slot lane%4)
-  const int lr = lane >> 2, ps = lane & 3;
-  const u16* asrc[2];
+  // DMA sources: instruction i of a plane covers RPI rows x RB bytes; lane -> (row i * RPI + lane / LPR, slot lane % LPR)
+  const int lr = lane / LPR, ps = lane % LPR;
+  const u16* asrc[AIW];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {  // A: 8 instructions per plane, 2 per wave
-    const int r = (wave + 4 * j) * 16 + lr;
-    const int kq = ps ^ ((r >> 2) & 2);
-    asrc[j] = P.a + (int64_t)min(m0 + r, P.M - 1) * P.K + kq * 8;
+  for (int j = 0; j < AIW; ++j) {
+    const int r = (wave + 4 * j) * RPI + lr;
+    asrc[j] = P.a + (int64_t)min(m0 + r, P.M - 1) * P.K + swz(ps, r) * 8;
   }
-  const u16* bsrc[3];
+  const u16* bsrc[BIW];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {  // B: 12 instructions per plane, 3 per wave
-    const int r = (wave + 4 * j) * 16 + lr;
-    const int kq = ps ^ ((r >> 2) & 2);
-    bsrc[j] = P.w + (int64_t)(n0 + r) * P.kpad + kq * 8;
+  for (int j = 0; j < BIW; ++j) {
+    const int r = (wave + 4 * j) * RPI + lr;
+    bsrc[j] = P.w + (int64_t)(n0 + r) * P.kpad + swz(ps, r) * 8;
   }
   auto stage = [&](int ks, int buf) {
     char* base = smem + buf * STAGE;
-    const int k0 = ks * 32;
+    const int k0 = ks * KD;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < AIW; ++j) {
       sg_glds16(asrc[j] + k0, base + (wave + 4 * j) * 1024);
       sg_glds16(asrc[j] + P.a_lo + k0, base + AB + (wave + 4 * j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < BIW; ++j) {
       sg_glds16(bsrc[j] + k0, base + 2 * AB + (wave + 4 * j) * 1024);
       sg_glds16(bsrc[j] + P.w_lo + k0, base + 2 * AB + BB + (wave + 4 * j) * 1024);
     }
@@ -100,46 +109,50 @@ __global__ __launch_bounds__(256, 1) void sgemm_planes_kernel(const SGemmDev P) 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = P.K / 32;
-  // fragment geometry: lane reads row (lane & 15) of a 16-row block, chunk lane >> 4
+  const int nk = P.K / KD;
+  // fragment geometry: lane reads row (lane & 15) of a 16-row block, chunk (4 sub + lane >> 4); 16-row blocks keep the
+  // swizzle, so block i is + i * 16 rows
   const int fr = lane & 15, fq = lane >> 4;
-  const int aoff = (wm * 64 + fr) * 64 + ((fq ^ (((wm * 64 + fr) >> 2) & 2)) << 4);
-  const int boff = (wn * 96 + fr) * 64 + ((fq ^ (((wn * 96 + fr) >> 2) & 2)) << 4);
-  // ring of SG_STAGES stages, two ahead: 10 DMA instructions per wave per stage
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int ar = wm * 64 + fr, br = wn * 96 + fr;
+  // ring of NST stages, NST - 1 ahead
+#pragma unroll
+  for (int d = 0; d < NST - 1; ++d)
+    if (d < nk) stage(d, d);
+  if (nk > NST - 2 && NST > 2) __builtin_amdgcn_s_waitcnt(((NST - 2) * DPW & 15) | (7 << 4) | (((NST - 2) * DPW >> 4) << 14));
+  else __builtin_amdgcn_s_waitcnt((7 << 4));  // vmcnt(0)
   __builtin_amdgcn_s_barrier();
   for (int ks = 0; ks < nk; ++ks) {
-    const bool more = ks + 2 < nk;
-    if (more) stage(ks + 2, (ks + 2) % SG_STAGES);
-    const char* base = smem + (ks % SG_STAGES) * STAGE;
-    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
-    // (16-row blocks keep (row >> 2) & 2, so the swizzled offset of block i is aoff + i * 16 rows)
+    const bool more = ks + NST - 1 < nk;
+    if (more) stage(ks + NST - 1, (ks + NST - 1) % NST);
+    const char* base = smem + (ks % NST) * STAGE;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      ah[i] = *reinterpret_cast<const bf16x8*>(base + aoff + i * 1024);
-      al[i] = *reinterpret_cast<const bf16x8*>(base + AB + aoff + i * 1024);
-    }
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int aoff = ar * RB + (swz(4 * sb + fq, ar) << 4), boff = br * RB + (swz(4 * sb + fq, br) << 4);
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      bh[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + boff + j * 1024);
-      bl[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + BB + boff + j * 1024);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(base + aoff + i * 16 * RB);
+        al[i] = *reinterpret_cast<const bf16x8*>(base + AB + aoff + i * 16 * RB);
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        acc[i][j] = mfma16<PREC_BF16>(al[i], bh[j], acc[i][j]);
-        acc[i][j] = mfma16<PREC_BF16>(ah[i], bl[j], acc[i][j]);
-        acc[i][j] = mfma16<PREC_BF16>(ah[i], bh[j], acc[i][j]);
+        bh[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + boff + j * 16 * RB);
+        bl[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + BB + boff + j * 16 * RB);
       }
-    __builtin_amdgcn_s_setprio(0);
-    // stage ks + 1 has landed; stage ks + 2 stays in flight across the barrier
-    if (more) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = mfma16<PREC_BF16>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_BF16>(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16<PREC_BF16>(ah[i], bh[j], acc[i][j]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // stage ks + 1 has landed; younger stages stay in flight across the barrier
+    if (more && NST > 2) __builtin_amdgcn_s_waitcnt(((NST - 2) * DPW & 15) | (7 << 4) | (((NST - 2) * DPW >> 4) << 14));
+    else __builtin_amdgcn_s_waitcnt((7 << 4));  // vmcnt(0) lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
   }
 
@@ -222,6 +235,7 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 }
 
 bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K && knobs().sgemm; }
+static int sg_variant(int K) { return knobs().sgemm == 2 && K % 64 == 0 ? 2 : (knobs().sgemm == 3 ? 3 : 1); }
 
 int sgemm_planes(const u16* a, int64_t a_lo, int M, int K, const u16* w, int64_t w_lo, int kpad, int N,
                  const float* bias, const float* res, int64_t ldr, float* out, int64_t ldo, float out_scale,
@@ -241,10 +255,14 @@ int sgemm_planes(const u16* a, int64_t a_lo, int M, int K, const u16* w, int64_t
   if (nwg >= (1ll << 30)) return set_error(ALCM_E_INVALID, "sgemm_planes: problem too large");
   P.nwg = (int)nwg;
   void* tok = prof_start(s);
-  hipLaunchKernelGGL(sgemm_planes_kernel, dim3((unsigned)nwg), dim3(256), 0, s, P);
+  const int v = sg_variant(K);
+  if (v == 2) hipLaunchKernelGGL((sgemm_planes_kernel<64, 2, 1>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+  else if (v == 3) hipLaunchKernelGGL((sgemm_planes_kernel<32, 2, 2>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+  else hipLaunchKernelGGL((sgemm_planes_kernel<32, 3, 1>), dim3((unsigned)nwg), dim3(256), 0, s, P);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::sgemm_planes_kernel");
+    std::snprintf(name, sizeof(name), "alcm::sgemm_planes_kernel<%d, %d, %d>", v == 2 ? 64 : 32, v == 1 ? 3 : 2,
+                  v == 3 ? 2 : 1);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " M%d N%d K%d", M, N, K);
     const double flops = 2.0 * M * N * (double)K;

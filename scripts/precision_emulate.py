@@ -132,6 +132,14 @@ def main():
             cases["mixed(s3 F16) + ups0-2 F16"] = dict(base2, **wide_ups)
             cases["mixed(s3 F16) + ups0-2 F16, ups3-5 F16W2"] = dict(base2, ups=("f16", "f32"), **wide_ups)
             cases["mixed(s3 F16) + ups0-3 F16"] = dict(base2, ups3=("f16", "f16"), **wide_ups)
+        if len(sys.argv) > 2 and sys.argv[2] == "ups45":  # stage 4-5 upsamplers on fp16 activations (current mixed base)
+            base = dict({"wide": ("f16", "f16"), "tail": ("f16", "f32"), "s3": ("f16", "f16"), "fir_wide": ("f16", "f32")},
+                        **{f"ups{i}": ("f16", "f16") for i in range(4)})
+            cases = {"mixed policy (round 4)": base,
+                     "mixed + ups4 F16W2": dict(base, ups4=("f16", "f32")),
+                     "mixed + ups5 F16W2": dict(base, ups5=("f16", "f32")),
+                     "mixed + ups4,5 F16W2": dict(base, ups4=("f16", "f32"), ups5=("f16", "f32")),
+                     "mixed + ups4,5 bf16x3-free F16": dict(base, ups4=("f16", "f16"), ups5=("f16", "f16"))}
         for name, pol in cases.items():
             for ws in ((False, True) if any(v[1] == "f16" for v in pol.values()) else (False,)):
                 out = run(W, mel, pol, wscale=ws)
