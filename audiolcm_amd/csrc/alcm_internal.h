@@ -82,6 +82,10 @@ int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, 
            int accumulate, bool last, const float* ae1, const float* ib1, const Taps12O& f1, const float* ae2,
            const float* ib2, const Taps12O& f2, int prec, hipStream_t s);
 
+// BigVGAN stride-2 / kernel-4 upsampler, both phases in one split-precision pass (alcm_ups.hip)
+bool ups2_supported(int cin, int cout, int cpad, int rate, int taps);
+int ups2(const float* x, float* out, int B, int T, int cin, int cout, const unsigned short* w0, const unsigned short* w1,
+         int64_t lo, int kpad, const int pad[2], const int off[2], const float* bias, hipStream_t s);
 // bf16x3 1x1 conv on split operand planes (alcm_sgemm.hip)
 bool sgemm_planes_ok(int K, int N, int kpad);
 int sgemm_planes(const unsigned short* a, int64_t a_lo, int M, int K, const unsigned short* w, int64_t w_lo, int kpad,
@@ -117,7 +121,8 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
-  int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip; 1 / 2 / 3 = kernel variant), 0 = gemm_kernel
+  int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs
+  int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
   bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)
   int tconv_stagger = -1;        // ALCM_TCONV_STAGGER: streamed narrow conv grid: -1 by shape, 0 one workgroup per tile, >= 1 persistent (stagger - 1 sleeps)

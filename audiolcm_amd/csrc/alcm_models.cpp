@@ -1459,7 +1459,14 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
                             (wide_ok || (S.cout <= 96 && S.cout % 4 == 0)) &&
                             S.phase[0].w.cpad == S.cin && !knobs().ups_fp32;
     if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
-    for (int r = 0; r < S.rate; ++r) {
+    // the split-precision stride-2 stages with the kernel's widths (stages 4-5): both phases in one pass over x
+    const bool ups_two = !ups_planes && split == PREC_SPLIT && S.rate == 2 &&
+                         ups2_supported(S.cin, S.cout, S.phase[0].w.cpad, S.rate, S.phase[0].w.taps) &&
+                         S.phase[1].w.kpad == S.phase[0].w.kpad && S.phase[1].w.lo == S.phase[0].w.lo;
+    if (ups_two)
+      ALCM_TRY(ups2(x, u, B, T, S.cin, S.cout, S.phase[0].w.p, S.phase[1].w.p, S.phase[0].w.lo, S.phase[0].w.kpad,
+                    S.pad.data(), S.off.data(), S.phase[0].b, s));
+    for (int r = 0; r < S.rate && !ups_two; ++r) {
       if (ups_planes) {
         const ConvW& cw = S.phase[r];
         alcm_opconv_args g;

@@ -9,10 +9,8 @@
 // registers: 147 us per DiT proj launch (M = 14944, N = K = 576) against an MFMA floor of 12 us.
 //
 // Structure: 128 x 192 output tile, 4 waves as 2 (M) x 2 (N) of 64 x 96 (16x16x32 MFMAs), 32-deep K stages of
-// both planes of both operands (16 + 24 KB) DMA'd two stages ahead into a 3-stage ring (global_load_lds, rows of
-// 64 B with the 16-B chunk kq of row r at slot kq ^ ((r >> 2) & 2): conflict-free ds_read_b128; counted vmcnt,
-// raw barriers); the epilogue stages 64-row halves of the tile through LDS for whole-row float4 residual loads and
-// stores.
+// both planes of both operands (16 + 24 KB) by LDS-DMA (global_load_lds) into a stage ring, two workgroups per CU;
+// the epilogue stages 64-row halves of the tile through LDS for whole-row float4 residual loads and stores.
 #include <cstdio>
 #include <cstring>
 
@@ -45,10 +43,12 @@ __device__ __forceinline__ void sg_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
 }
 
-// Variants (ALCM_SGEMM: 1 = KD 32, 3 stages, one workgroup per CU; 2 = KD 64 (whole 128-B row segments per DMA
-// lane group), 2 stages, one per CU; 3 = KD 32, 2 stages, two workgroups per CU).  KD-deep K stages of both planes of
-// both operands are DMA'd NST - 1 stages ahead into an NST-stage ring; rows of KD * 2 bytes, the 16-B chunk kq of row r
-// at slot kq ^ (r & 7) (KD 64) / kq ^ ((r >> 2) & 2) (KD 32): conflict-free ds_read_b128
+// KD-deep K stages of both planes of both operands are DMA'd NST - 1 stages ahead into an NST-stage ring; rows of
+// KD * 2 bytes, the 16-B chunk kq of row r at slot kq ^ (r & 7) (KD 64) / kq ^ ((r >> 2) & 2) (KD 32): conflict-free
+// ds_read_b128.  Built as KD 32, 2 stages, two workgroups per CU (80 KB each): against 3 stages at one per CU and
+// against 64-deep stages (whole 128-B row segments) at one per CU, per step 1.69 vs 2.23 / 2.12 ms over the 120
+// launches (DiT proj_in / proj_out 0.94 vs 1.26 / 1.21; bit-identical; +0.6 % end to end, profiles/r4m) — the DiT
+// shape's 351 tiles then run in one round instead of 1.4, and the co-resident workgroup hides the DMA waits
 template <int KD, int NST, int OCC>
 __global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P) {
   constexpr int TM = 4, TN = 6;
@@ -235,7 +235,7 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 }
 
 bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K && knobs().sgemm; }
-static int sg_variant(int K) { return knobs().sgemm == 2 && K % 64 == 0 ? 2 : (knobs().sgemm == 3 ? 3 : 1); }
+
 
 int sgemm_planes(const u16* a, int64_t a_lo, int M, int K, const u16* w, int64_t w_lo, int kpad, int N,
                  const float* bias, const float* res, int64_t ldr, float* out, int64_t ldo, float out_scale,
@@ -255,14 +255,10 @@ int sgemm_planes(const u16* a, int64_t a_lo, int M, int K, const u16* w, int64_t
   if (nwg >= (1ll << 30)) return set_error(ALCM_E_INVALID, "sgemm_planes: problem too large");
   P.nwg = (int)nwg;
   void* tok = prof_start(s);
-  const int v = sg_variant(K);
-  if (v == 2) hipLaunchKernelGGL((sgemm_planes_kernel<64, 2, 1>), dim3((unsigned)nwg), dim3(256), 0, s, P);
-  else if (v == 3) hipLaunchKernelGGL((sgemm_planes_kernel<32, 2, 2>), dim3((unsigned)nwg), dim3(256), 0, s, P);
-  else hipLaunchKernelGGL((sgemm_planes_kernel<32, 3, 1>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+  hipLaunchKernelGGL((sgemm_planes_kernel<32, 2, 2>), dim3((unsigned)nwg), dim3(256), 0, s, P);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::sgemm_planes_kernel<%d, %d, %d>", v == 2 ? 64 : 32, v == 1 ? 3 : 2,
-                  v == 3 ? 2 : 1);
+    std::snprintf(name, sizeof(name), "alcm::sgemm_planes_kernel<32, 2, 2>");
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " M%d N%d K%d", M, N, K);
     const double flops = 2.0 * M * N * (double)K;
