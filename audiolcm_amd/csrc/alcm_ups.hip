@@ -6,11 +6,12 @@
 // fp32-operand GEMM launches (alcm_gemm.hip), each re-reading x and converting it to bf16 hi / lo per 32-deep K step
 // per N tile: 0.31 + 0.54 ms per phase pair at stages 4 / 5 against 0.09 of HBM time.
 //
-// Structure: one persistent 512-thread workgroup per CU, both phases' packed bf16 hi / lo weight planes resident in
+// Structure: persistent 512-thread workgroups (one per CU at stage 4, two at stage 5), both phases' packed bf16 hi / lo weight planes resident in
 // LDS (rows of an odd number of 16-B slots); per tile of TM = 128 input rows the window [t0 - 1, t0 + 129) is split
-// into bf16 hi / lo operand rows in LDS (channels cin .. cp - 1 zero, rows outside [0, T) zero = the conv padding),
+// into bf16 hi / lo operand rows in LDS (rows outside [0, T) zero = the conv padding),
 // while the next tile's window is already loading into registers; wave w computes input rows 16 w .. 16 w + 15 of
-// both phases (bf16x3: lo*hi + hi*lo + hi*hi per 32-deep K slice, K = tap * cp + c as the packed weights) and stores
+// both phases (bf16x3: lo*hi + hi*lo + hi*hi per 32-deep K slice, K = tap * cp + c as the packed weights, cp = cin: a
+// lane's 8 channels never straddle a tap) and stores
 // its fp32 outputs straight from the accumulators.
 #include <cstdio>
 #include <cstring>
@@ -49,11 +50,12 @@ struct UpsGeo {
   static constexpr int WPL = NOUT * WRS;                         // one weight plane
   static constexpr int WB = (4 * WPL + 1023) / 1024 * 1024;      // [phase][plane][row]
   static constexpr int SMEM = WB + 2 * XPL;
-  static_assert(CP % 32 == 0 && NOUT % 16 == 0 && SMEM <= 163840, "geometry");
+  static constexpr int OCC = SMEM <= 81920 ? 2 : 1;             // workgroups per CU (stage 5: two)
+  static_assert(KD % 32 == 0 && CP % 8 == 0 && NOUT % 16 == 0 && SMEM <= 163840, "geometry");
 };
 
 template <int CP, int NOUT, int CIN>
-__global__ __launch_bounds__(512, 1) void ups2_kernel(const Ups2Dev P) {
+__global__ __launch_bounds__(512, UpsGeo<CP, NOUT>::OCC) void ups2_kernel(const Ups2Dev P) {
   using G = UpsGeo<CP, NOUT>;
   constexpr int TM = G::TM, TR = G::TR, NT = G::NT, XRS = G::XRS, WRS = G::WRS, KD = G::KD;
   constexpr int NTN = NOUT / 16, NS = KD / 32;
@@ -188,12 +190,12 @@ __global__ __launch_bounds__(512, 1) void ups2_kernel(const Ups2Dev P) {
 // ------------------------------------------------------------------------------------------------------ host
 bool ups2_supported(int cin, int cout, int cpad, int rate, int taps) {
   if (!knobs().ups2 || rate != 2 || taps != 2) return false;
-  return (cin == 96 && cpad == 96 && cout == 48) || (cin == 48 && cpad == 64 && cout == 24);
+  return (cin == 96 && cpad == 96 && cout == 48) || (cin == 48 && cpad == 48 && cout == 24);
 }
 
 int ups2(const float* x, float* out, int B, int T, int cin, int cout, const u16* w0, const u16* w1, int64_t lo,
          int kpad, const int pad[2], const int off[2], const float* bias, hipStream_t s) {
-  const int cpad = cin == 96 ? 96 : 64;
+  const int cpad = cin;
   if (!ups2_supported(cin, cout, cpad, 2, 2)) return set_error(ALCM_E_INVALID, "ups2: unsupported shape");
   if (!x || !out || !w0 || !w1 || !bias || B <= 0 || T <= 0 || kpad < 2 * cpad || (((uintptr_t)x) & 15) ||
       (((uintptr_t)w0) & 15) || (((uintptr_t)w1) & 15) || (lo % 8) || (kpad % 8))
@@ -218,10 +220,10 @@ int ups2(const float* x, float* out, int B, int T, int cin, int cout, const u16*
               ? n
               : 256;
   }
-  const int grid = (int)std::min<int64_t>(nt, ncu);
+  const int grid = (int)std::min<int64_t>(nt, (int64_t)ncu * (cin == 96 ? UpsGeo<96, 48>::OCC : UpsGeo<48, 32>::OCC));
   void* tok = prof_start(s);
   if (cin == 96) hipLaunchKernelGGL((ups2_kernel<96, 48, 96>), dim3(grid), dim3(512), 0, s, P);
-  else hipLaunchKernelGGL((ups2_kernel<64, 32, 48>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((ups2_kernel<48, 32, 48>), dim3(grid), dim3(512), 0, s, P);
   ALCM_HIP(hipGetLastError());
   if (tok) {
     const double M = (double)B * T;
