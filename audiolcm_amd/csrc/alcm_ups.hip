@@ -55,7 +55,7 @@ struct UpsGeo {
 };
 
 template <int CP, int NOUT, int CIN>
-__global__ __launch_bounds__(512, UpsGeo<CP, NOUT>::OCC) void ups2_kernel(const Ups2Dev P) {
+__global__ __launch_bounds__(512, (UpsGeo<CP, NOUT>::OCC)) void ups2_kernel(const Ups2Dev P) {
   using G = UpsGeo<CP, NOUT>;
   constexpr int TM = G::TM, TR = G::TR, NT = G::NT, XRS = G::XRS, WRS = G::WRS, KD = G::KD;
   constexpr int NTN = NOUT / 16, NS = KD / 32;
