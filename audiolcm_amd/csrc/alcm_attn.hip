@@ -17,6 +17,7 @@
 // to the fp32 output.
 #include <cmath>
 #include <cstdio>
+#include <type_traits>
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
@@ -194,6 +195,8 @@ constexpr int FR_MAXL = 512;   // keys padded to a multiple of 64
 constexpr int FR_KS = 80;      // K row stride (elements, 160 B): conflict-free ds_read_b128; dims dh..79 zero
 constexpr int FR_MAXDH = 72;
 constexpr int FR_THREADS = 1024;  // 16 waves: 4 per SIMD hide the per-tile softmax / LDS latency chain
+// (round 4: scores in the log2 domain (q pre-scaled), exp2 straight to v_exp_f32, masking only in the last key tile,
+// the running-output rescale skipped when no query's max moved)
 
 template <int PREC>
 __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float* __restrict__ qkv, float* __restrict__ O,
@@ -246,6 +249,8 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
   __syncthreads();
 
   const int nqb = (L + 15) / 16, nkt = Lp / FA_KT;
+  // q pre-scaled by scale * log2(e): the scores come out in the log2 domain and p = exp2(s - m) is one v_exp_f32
+  const float qs = scale * 1.44269504088896341f;
   for (int qb = wave; qb < nqb; qb += FR_THREADS / 64) {
     const int q0 = qb * 16;
     // (branch-free: clamped addresses and selects; exec-masked loads inside this loop serialise it)
@@ -261,7 +266,7 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
         for (int j = 0; j < 8; ++j) {
           const int d = 32 * ks + 8 * g + j;
           const float v = qr[d < dh ? d : 0];
-          e[j] = fa_cvt<PREC>((qok && d < dh) ? v : 0.f);
+          e[j] = fa_cvt<PREC>((qok && d < dh) ? v * qs : 0.f);
         }
         qf[ks] = __builtin_bit_cast(bf16x8, e);
       }
@@ -296,33 +301,42 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
           s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
         }
       }
+      if (k0 + FA_KT > L) {  // (wave-uniform) only the last tile has keys >= L
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 16 * kb + 4 * g + r;
+            s[kb][r] = key < L ? s[kb][r] : -INFINITY;
+          }
+      }
       float tmax = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * kb + 4 * g + r;
-          const float v = key < L ? s[kb][r] * scale : -INFINITY;
-          s[kb][r] = v;
-          tmax = fmaxf(tmax, v);
-        }
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[kb][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
       const float mn = fmaxf(m, tmax);
-      const float alpha = __expf(m - mn);
-      m = mn;
+      // rescale only when some query's running max moved (wave-uniform branch; lanes whose max did not move
+      // scale by exactly 1)
+      if (__any(mn != m)) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[i] *= alpha;
+        m = mn;
+      }
       float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = __expf(s[kb][r] - mn);
+          const float pv = __builtin_amdgcn_exp2f(s[kb][r] - m);
           s[kb][r] = pv;
           psum += pv;
         }
-      l = l * alpha + psum;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) o[i] *= alpha;
+      l += psum;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         u16 pe[8];

@@ -32,7 +32,8 @@ int group_norm_affine(const float* x, int B, int T, int C, int64_t sb, int64_t s
                       const float* gamma, const float* beta, float* scale, float* shift, hipStream_t s);
 int row_stats(const float* x, int rows, int C, int64_t ld, float eps, float* mean, float* rstd, hipStream_t s);
 int layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const float* gamma, const float* beta,
-               const float* add, int64_t ld_add, float* y, int64_t ld_out, hipStream_t s);
+               const float* add, int64_t ld_add, float* y, int64_t ld_out, hipStream_t s, int rpb = 0,
+               int64_t out_bs = 0);
 int softmax_rows(float* x, int rows, int n, int64_t ld, hipStream_t s);
 int layer_norm_plane(const float* x, int rows, int C, int64_t ld, float eps, const float* gamma, const float* beta,
                      void* plane, int prec, hipStream_t s);

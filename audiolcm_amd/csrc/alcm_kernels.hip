@@ -77,7 +77,7 @@ template <bool APPLY>
 __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, int rows, int C, int64_t ld, float eps,
                                                  float* mean_out, float* rstd_out, const float* __restrict__ gamma,
                                                  const float* __restrict__ beta, const float* __restrict__ add,
-                                                 int64_t ld_add, float* y, int64_t ld_out) {
+                                                 int64_t ld_add, float* y, int64_t ld_out, int rpb, int64_t out_bs) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -99,8 +99,16 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, in
     }
     return;
   }
-  float* yr = y + (int64_t)row * ld_out;
-  const float* ar = add ? add + (int64_t)row * ld_add : nullptr;
+  // rpb > 0: rows come in batches of rpb; the add row is the row within its batch, output batch bb starts at row
+  // bb * out_bs (the DiT condition tokens: one launch for every clip, written into the [B][CT] token rows)
+  int64_t arow = row, orow = row;
+  if (rpb > 0) {
+    const int bb = row / rpb, t = row - bb * rpb;
+    arow = t;
+    orow = (int64_t)bb * out_bs + t;
+  }
+  float* yr = y + orow * ld_out;
+  const float* ar = add ? add + arow * ld_add : nullptr;
   for (int c = lane; c < C; c += 64) {
     float o = (xr[c] - mean) * rstd * gamma[c] + beta[c];
     if (ar) o += ar[c];
@@ -111,16 +119,16 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, in
 int row_stats(const float* x, int rows, int C, int64_t ld, float eps, float* mean, float* rstd, hipStream_t s) {
   if (!x || !mean || !rstd || rows <= 0 || C <= 0) return set_error(ALCM_E_INVALID, "row_stats: bad arguments");
   hipLaunchKernelGGL(ln_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, ld, eps, mean, rstd,
-                     nullptr, nullptr, nullptr, (int64_t)0, nullptr, (int64_t)0);
+                     nullptr, nullptr, nullptr, (int64_t)0, nullptr, (int64_t)0, 0, (int64_t)0);
   ALCM_HIP(hipGetLastError());
   return 0;
 }
 
 int layer_norm(const float* x, int rows, int C, int64_t ld_in, float eps, const float* gamma, const float* beta,
-               const float* add, int64_t ld_add, float* y, int64_t ld_out, hipStream_t s) {
-  if (!x || !y || !gamma || !beta || rows <= 0 || C <= 0) return set_error(ALCM_E_INVALID, "layer_norm: bad arguments");
+               const float* add, int64_t ld_add, float* y, int64_t ld_out, hipStream_t s, int rpb, int64_t out_bs) {
+  if (!x || !y || !gamma || !beta || rows <= 0 || C <= 0 || rpb < 0) return set_error(ALCM_E_INVALID, "layer_norm: bad arguments");
   hipLaunchKernelGGL(ln_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, C, ld_in, eps, nullptr, nullptr,
-                     gamma, beta, add, ld_add, y, ld_out);
+                     gamma, beta, add, ld_add, y, ld_out, rpb, out_bs);
   ALCM_HIP(hipGetLastError());
   return 0;
 }

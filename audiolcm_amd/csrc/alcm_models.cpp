@@ -773,10 +773,10 @@ static int dit_embed_context(alcm_model* m, const float* ctx, int B, float* cemb
     o1.act = ACT_GELU_TANH;
     ALCM_TRY(conv(s, prec_of(m, false), B, n, x, D.c0[e], ocl(t0, n, H), o1));
     ALCM_TRY(conv(s, prec_of(m, false), B, n, cl(t0, n, H), D.c2[e], ocl(t1, n, H), ConvOpts{}));
-    // LayerNorm, plus the learned position rows 1+e*n .. (PositionEmbedding MODE_ADD, new_attention.py:245-248)
-    for (int b = 0; b < B; ++b)
-      ALCM_TRY(layer_norm(t1 + (int64_t)b * n * H, n, H, H, 1e-5f, D.cln[e].g, D.cln[e].b,
-                          D.pos + (int64_t)(1 + e * n) * H, H, cemb + ((int64_t)b * CT + e * n) * H, H, s));
+    // LayerNorm, plus the learned position rows 1+e*n .. (PositionEmbedding MODE_ADD, new_attention.py:245-248),
+    // one launch for all clips: row b * n + t -> token row b * CT + e * n + t
+    ALCM_TRY(layer_norm(t1, B * n, H, H, 1e-5f, D.cln[e].g, D.cln[e].b, D.pos + (int64_t)(1 + e * n) * H, H,
+                        cemb + (int64_t)e * n * H, H, s, n, CT));
   }
   return 0;
 }
