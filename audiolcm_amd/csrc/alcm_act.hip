@@ -32,12 +32,18 @@ __device__ __forceinline__ f32x2 ld_f32x2(const float* base, uint32_t byte_off) 
   return *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
-template <int PREC, int AC_NP>
-__global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__ x, u16* __restrict__ y,
-                                                       int64_t y_lo, int T, int C, int Cp,
-                                                       const float* __restrict__ aexp,
-                                                       const float* __restrict__ ibeta, const Taps12O f,
-                                                       int tiles_t, int tiles_c) {
+// NSET parameter sets over the same input (the three resblocks' first Activation1d of a BigVGAN stage: the x window
+// is loaded once, then per set phase 1 -> barrier -> phase 2 into that set's planes)
+struct ActSets {
+  u16* y[3];
+  const float* aexp[3];
+  const float* ibeta[3];
+};
+
+template <int PREC, int AC_NP, int NSET>
+__global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__ x, const ActSets S, int64_t y_lo,
+                                                       int T, int C, int Cp, const Taps12O f, int tiles_t,
+                                                       int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
   constexpr int AC_TT = 2048 / AC_NP;             // output rows per tile (8 per phase-2 thread)
   constexpr int NSEG = 256 / AC_NP;                // phase-1 segments
@@ -59,86 +65,98 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   // each load / store is a saddr + 32-bit voffset access instead of a 64-bit multiply-add per address
   const float* xb = x + ((int64_t)b * T) * C;
   const int xc = live ? c : 0;
-  const f32x2 ear = live ? f32x2{aexp[c], aexp[c + 1]} * INV_PI : f32x2{0.f, 0.f};
-  const f32x2 h = live ? f32x2{ibeta[c], ibeta[c + 1]} * 0.5f : f32x2{0.f, 0.f};
   const int m0 = 2 * t0 - 6;  // sample index 0 of the tile (even); output j reads m = 2j - 5 .. 2j + 6
-
-  // ---- phase 1: upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
-  //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
-  if (live) {
-    const int seg = tid / AC_NP;
-    const int mb = m0 + seg * AC_SEG;
-    const int xlo = mb / 2 - 3;  // sample mb + q reads x rows xlo + (q + 5 - ku) / 2 + 3 - 3
-    if (mb >= 0 && mb + AC_SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1) {
-      f32x2 win[15];
-      const uint32_t o0 = (uint32_t)(xlo * C + xc);
+  const int seg = tid / AC_NP;
+  const int mb = m0 + seg * AC_SEG;
+  const int xlo = mb / 2 - 3;  // sample mb + q reads x rows xlo + (q + 5 - ku) / 2 + 3 - 3
+  const bool interior = mb >= 0 && mb + AC_SEG - 1 <= 2 * T - 1 && xlo >= 0 && xlo + 14 <= T - 1;
+  f32x2 win[15];
+  if (live && interior) {
+    const uint32_t o0 = (uint32_t)(xlo * C + xc);
 #pragma unroll
-      for (int i = 0; i < 15; ++i) win[i] = ld_f32x2(xb, (o0 + (uint32_t)(i * C)) * 4u);
-      // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
-      // order compiles to 6-deep dependent chains with a wait state between links)
-      f32x2 u[AC_SEG];
-#pragma unroll
-      for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 6; ++kk)
-#pragma unroll
-        for (int q = 0; q < AC_SEG; ++q) {
-          const int ku = 2 * kk + ((q & 1) ? 0 : 1);
-          u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
-        }
-#pragma unroll
-      for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
-    } else {
-      for (int q = 0; q < AC_SEG; ++q) {
-        int m = mb + q;
-        m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
-        f32x2 u = f32x2{0.f, 0.f};
-        for (int kk = 0; kk < 6; ++kk) {
-          const int ku = 2 * kk + ((m & 1) ? 0 : 1);
-          int xi = (m + 5 - ku) / 2;
-          xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
-          u = fma2(f32x2{f.up[ku], f.up[ku]}, ld_f32x2(xb, (uint32_t)(xi * C + xc) * 4u), u);
-        }
-        sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
-      }
-    }
+    for (int i = 0; i < 15; ++i) win[i] = ld_f32x2(xb, (o0 + (uint32_t)(i * C)) * 4u);
   }
-  __syncthreads();
-  // ---- phase 2: outputs j0 .. j0 + 7 of pair p: o[j] = sum_k dn[k] * sv[2j + k - 5 - m0]
   const int run = tid / AC_NP;
   const int j0 = t0 + run * 8;
-  if (j0 >= T) return;
-  u16* yb = y + ((int64_t)b * T) * Cp;
   const int jn = min(8, T - j0);
-  if (!live) {
-    for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (uint32_t)((j0 + r) * Cp + c), y_lo, f32x2{0.f, 0.f});
-    return;
-  }
-  const f32x2* sp = sv + (2 * (j0 - t0) + 1) * AC_RS + p;
-  f32x2 s[26];
+
 #pragma unroll
-  for (int i = 0; i < 26; ++i) s[i] = sp[i * AC_RS];
-  // tap-outer: 8 independent chains (one per output, each summed in ascending tap order like the fused
-  // epilogue's), then the stores (no per-row branch between the chains)
-  f32x2 o[8];
+  for (int st = 0; st < NSET; ++st) {
+    const f32x2 ear = live ? f32x2{S.aexp[st][c], S.aexp[st][c + 1]} * INV_PI : f32x2{0.f, 0.f};
+    const f32x2 h = live ? f32x2{S.ibeta[st][c], S.ibeta[st][c + 1]} * 0.5f : f32x2{0.f, 0.f};
+    // ---- phase 1: upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
+    //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
+    if (live) {
+      if (interior) {
+        // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
+        // order compiles to 6-deep dependent chains with a wait state between links)
+        f32x2 u[AC_SEG];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) o[r] = f32x2{0.f, 0.f};
+        for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < 12; ++k)
+        for (int kk = 0; kk < 6; ++kk)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, s[2 * r + k], o[r]);
-  const uint32_t yo = (uint32_t)(j0 * Cp + c) * 2u;  // byte offset from the uniform batch base
-  auto yp = [&](int r) { return reinterpret_cast<u16*>(reinterpret_cast<char*>(yb) + (yo + (uint32_t)(r * Cp) * 2u)); };
-  if (jn == 8) {
+          for (int q = 0; q < AC_SEG; ++q) {
+            const int ku = 2 * kk + ((q & 1) ? 0 : 1);
+            u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
+          }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
-  } else {
-    for (int r = 0; r < jn; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
+        for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
+      } else {
+        for (int q = 0; q < AC_SEG; ++q) {
+          int m = mb + q;
+          m = m < 0 ? 0 : (m > 2 * T - 1 ? 2 * T - 1 : m);
+          f32x2 u = f32x2{0.f, 0.f};
+          for (int kk = 0; kk < 6; ++kk) {
+            const int ku = 2 * kk + ((m & 1) ? 0 : 1);
+            int xi = (m + 5 - ku) / 2;
+            xi = xi < 0 ? 0 : (xi > T - 1 ? T - 1 : xi);
+            u = fma2(f32x2{f.up[ku], f.up[ku]}, ld_f32x2(xb, (uint32_t)(xi * C + xc) * 4u), u);
+          }
+          sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u, ear, h);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: outputs j0 .. j0 + 7 of pair p: o[j] = sum_k dn[k] * sv[2j + k - 5 - m0]
+    if (j0 < T) {
+      u16* yb = S.y[st] + ((int64_t)b * T) * Cp;
+      if (!live) {
+        for (int r = 0; r < jn; ++r) op_store2<PREC>(yb + (uint32_t)((j0 + r) * Cp + c), y_lo, f32x2{0.f, 0.f});
+      } else {
+        const f32x2* sp = sv + (2 * (j0 - t0) + 1) * AC_RS + p;
+        f32x2 sr[26];
+#pragma unroll
+        for (int i = 0; i < 26; ++i) sr[i] = sp[i * AC_RS];
+        // tap-outer: 8 independent chains (one per output, each summed in ascending tap order like the fused
+        // epilogue's), then the stores (no per-row branch between the chains)
+        f32x2 o[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) o[r] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = fma2(f32x2{f.dn[k], f.dn[k]}, sr[2 * r + k], o[r]);
+        const uint32_t yo = (uint32_t)(j0 * Cp + c) * 2u;  // byte offset from the uniform batch base
+        auto yp = [&](int r) {
+          return reinterpret_cast<u16*>(reinterpret_cast<char*>(yb) + (yo + (uint32_t)(r * Cp) * 2u));
+        };
+        if (jn == 8) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
+        } else {
+          for (int r = 0; r < jn; ++r) op_store2<PREC>(yp(r), y_lo, o[r]);
+        }
+      }
+    }
+    if (st + 1 < NSET) __syncthreads();  // phase-2 reads of sv retired before the next set's phase 1
   }
 }
 
-int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
-             const Taps12O& f, int prec, hipStream_t s) {
+// nset parameter sets (1 or 3) of one input: y[i], alpha_exp[i], inv_beta[i]
+int act_coop(const float* x, void* const* y, int nset, int B, int T, int C, int Cp, const float* const* alpha_exp,
+             const float* const* inv_beta, const Taps12O& f, int prec, hipStream_t s) {
+  if (nset != 1 && nset != 3) return set_error(ALCM_E_INVALID, "activation1d: 1 or 3 parameter sets");
   // 64-channel tiles (whole 128-B output lines) measured faster at C = 768 (-15 %) and for the two-plane split
   // output (-10 %), slower at C = 384 (+10..15 %), even at C = 192 fp16 (scripts/microbench.py actnp)
   const int knp = knobs().act_np;
@@ -148,15 +166,26 @@ int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* 
   const int64_t nwg = (int64_t)B * tiles_t * tiles_c;
   if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
   const int64_t y_lo = (int64_t)B * T * Cp;
+  ActSets S{};
+  for (int i = 0; i < nset; ++i) {
+    S.y[i] = (u16*)y[i];
+    S.aexp[i] = alpha_exp[i];
+    S.ibeta[i] = inv_beta[i];
+  }
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
-                       tiles_t, tiles_c);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, S, y_lo, T, C, Cp, f, tiles_t, tiles_c);
   };
   auto pick = [&](auto npc) {
     constexpr int NP = decltype(npc)::value;
-    if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT, NP>);
-    else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16, NP>);
-    else launch(act_coop_kernel<PREC_F16, NP>);
+    if (nset == 3) {
+      if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT, NP, 3>);
+      else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16, NP, 3>);
+      else launch(act_coop_kernel<PREC_F16, NP, 3>);
+    } else {
+      if (prec == PREC_SPLIT) launch(act_coop_kernel<PREC_SPLIT, NP, 1>);
+      else if (prec == PREC_BF16) launch(act_coop_kernel<PREC_BF16, NP, 1>);
+      else launch(act_coop_kernel<PREC_F16, NP, 1>);
+    }
   };
   if (wide) pick(std::integral_constant<int, 32>{});
   else pick(std::integral_constant<int, 16>{});

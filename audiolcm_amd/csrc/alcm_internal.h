@@ -51,6 +51,9 @@ int to_planes(const float* x, void* y, int64_t rows, int C, int Cp, int prec, hi
 struct Taps12O;
 int act_conv_post(const float* x, float* wav, int B, int T, int C, const float* alpha_exp, const float* inv_beta,
                   const Taps12O& f, const float* w_tc, float bias, hipStream_t s);
+int activation1d_x3(const float* x, void* const y[3], int B, int T, int C, int Cp, const float* const alpha_exp[3],
+                    const float* const inv_beta[3], const float* up_filter, const float* down_filter, int prec,
+                    hipStream_t s);
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s);
@@ -122,6 +125,7 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
+  int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)
   int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs
   int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)

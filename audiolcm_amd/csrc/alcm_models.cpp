@@ -1496,6 +1496,19 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const bool pair = dense && stage_ampair(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
+    // the three chains' first Activation1d in one pass over u (their own planes, same taps; ALCM_ACT3=0: one per chain)
+    bool act3 = conc && fuse && !pair && S.rb.size() == 3 && knobs().act3 &&
+                !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
+    for (size_t j = 1; act3 && j < S.rb.size(); ++j)
+      act3 = !std::memcmp(S.rb[j].act[0].fup, S.rb[0].act[0].fup, sizeof(S.rb[0].act[0].fup)) &&
+             !std::memcmp(S.rb[j].act[0].fdn, S.rb[0].act[0].fdn, sizeof(S.rb[0].act[0].fdn));
+    if (act3) {
+      void* ys[3] = {w.ch[0].pl, w.ch[1].pl, w.ch[2].pl};
+      const float* ae[3] = {S.rb[0].act[0].aexp, S.rb[1].act[0].aexp, S.rb[2].act[0].aexp};
+      const float* ib[3] = {S.rb[0].act[0].ibeta, S.rb[1].act[0].ibeta, S.rb[2].act[0].ibeta};
+      ALCM_TRY(activation1d_x3(u, ys, B, To, S.cout, round_up(S.cout, 32), ae, ib, S.rb[0].act[0].fup,
+                               S.rb[0].act[0].fdn, pamp, s));
+    }
     if (conc) {  // chains start after the upsampler wrote u
       ALCM_HIP(hipEventRecord(ax->ev[0], s));
       for (auto a : ax->s) ALCM_HIP(hipStreamWaitEvent(a, ax->ev[0], 0));
@@ -1518,7 +1531,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
             nxt = nxt == cb.rb ? cb.t : cb.rb;
           }
         } else if (fuse) {
-          if (l == 0) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
+          if (l == 0 && !act3) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
                               &A.act[2 * l + 1], cb.pl2, dense));
           if (last) {

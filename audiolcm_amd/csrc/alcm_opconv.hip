@@ -23,8 +23,8 @@
 
 namespace alcm {
 
-int act_coop(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
-             const Taps12O& f, int prec, hipStream_t s);
+int act_coop(const float* x, void* const* y, int nset, int B, int T, int C, int Cp, const float* const* alpha_exp,
+             const float* const* inv_beta, const Taps12O& f, int prec, hipStream_t s);
 
 // sin(x)^2: Cody-Waite quadrant reduction + minimax sin/cos on |r| <= pi/4 (~1 ulp, branch-free)
 __device__ __forceinline__ float op_sin_sq(float x) {
@@ -91,6 +91,34 @@ __global__ __launch_bounds__(256) void act_op_kernel(const float* __restrict__ x
   }
 }
 
+// three Activation1d of one input with their own SnakeBeta parameters and the same FIR taps (a BigVGAN stage's three
+// resblocks' first half-layer): one cooperative pass, the input window loaded once (bit-identical to three calls)
+int activation1d_x3(const float* x, void* const y[3], int B, int T, int C, int Cp, const float* const alpha_exp[3],
+                    const float* const inv_beta[3], const float* up_filter, const float* down_filter, int prec,
+                    hipStream_t s) {
+  if (!x || !y[0] || !y[1] || !y[2] || !up_filter || !down_filter || B <= 0 || T <= 0 || C <= 0 || C % 2 ||
+      Cp < C || Cp % 32 || prec < PREC_BF16 || prec > PREC_F16W2 || (((uintptr_t)x) & 7))
+    return set_error(ALCM_E_INVALID, "activation1d_x3: bad arguments");
+  for (int i = 0; i < 3; ++i)
+    if (!alpha_exp[i] || !inv_beta[i] || (((uintptr_t)y[i]) & 3)) return set_error(ALCM_E_INVALID, "activation1d_x3: bad arguments");
+  if ((int64_t)B * T * Cp >= (1ll << 40)) return set_error(ALCM_E_INVALID, "activation1d_x3: problem too large");
+  Taps12O f;
+  for (int k = 0; k < 12; ++k) {
+    f.up[k] = 2.0f * up_filter[k];
+    f.dn[k] = down_filter[k];
+  }
+  void* tok = prof_start(s);
+  ALCM_TRY(act_coop(x, y, 3, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
+  if (tok) {
+    char name[64];
+    std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>, x3", prec == PREC_F16W2 ? PREC_F16 : prec);
+    const double e = (double)B * T;
+    prof_stop(tok, s, name, 3 * 2.0 * 36.0 * e * C, e * (4.0 * C + 3 * 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
+  }
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s) {
@@ -123,7 +151,10 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   }
   if (!knobs().act_v1) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
     void* tok = prof_start(s);
-    ALCM_TRY(act_coop(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
+    void* ys[1] = {y};
+    const float* ae[1] = {alpha_exp};
+    const float* ib[1] = {inv_beta};
+    ALCM_TRY(act_coop(x, ys, 1, B, T, C, Cp, ae, ib, f, prec, s));
     if (tok) {
       char name[64];
       std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>", prec == PREC_F16W2 ? PREC_F16 : prec);
