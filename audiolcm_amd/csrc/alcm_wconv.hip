@@ -646,10 +646,21 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   // persistent 8-wave kernel (ALCM_WCONV3: -1 by shape, 0 off, 1 wherever eligible): by shape where the 256-row
   // M tiles are >= 85 % full (BigVGAN T = 2496 / 9984 / 19968, DiT L = 467; not the VAE's T = 312, measured +15 %,
   // nor with the clips laid end to end as padded-flat rows: 2.85 vs 2.61 ms/step on wconv2)
+  // A persistent grid with fewer tiles than CUs leaves CUs idle where the two-workgroup kernel's half-size tiles share
+  // them: the DiT FFN down-projection (192 tiles of 256 x 192) measured 2.98 vs 2.82 ms/step (profiles/r4s)
   const int w3 = knobs().wconv3;
   const int mt256 = (a.T + W3_BM - 1) / W3_BM;
   const bool full = a.T * 100 >= mt256 * W3_BM * 85;
-  if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || full) && wconv3_try(a, wplane, flops, bytes, s))
+  if (!g_ncu) {
+    int dev = 0, n = 0;
+    g_ncu = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8)
+                ? n
+                : 256;
+  }
+  const bool fills = (int64_t)a.B * mt256 * (a.N / W3_BN) >= g_ncu;
+  if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || (full && fills)) &&
+      wconv3_try(a, wplane, flops, bytes, s))
     return 1;
   if (off && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
