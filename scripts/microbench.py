@@ -375,6 +375,25 @@ def bench_ampair(B=32):
             print(f"ampair C{C} k{k} d{d}: " + " ".join(res) + " ms", flush=True)
 
 
+def bench_text(B=32):
+    """Text encoders (BERT-base + CLAP Projection + T5-v1.1-large, mixed policy) at the bench batch: per-kernel rows of
+    one instrumented call (ALCM_PROF_SHAPES=1 splits them per shape) and the wall time per call."""
+    from audiolcm_amd.text_encoder import CLAPT5TextEncoder
+    enc = CLAPT5TextEncoder.from_recipe(0, split="mixed")
+    g = torch.Generator().manual_seed(7)
+    a = torch.randint(1, enc.cfg.b_vocab, (B, enc.cfg.max_len), generator=g)
+    b = torch.randint(1, enc.cfg.t_vocab, (B, enc.cfg.max_len), generator=g)
+    spin()
+    ms = timeit(lambda: enc.encode_ids(a, b), reps=10)
+    _hip.profile_begin()
+    enc.encode_ids(a, b)
+    torch.cuda.synchronize()
+    rows = sorted(_hip.profile_end(), key=lambda r: -r["total_ms"])
+    print(f"text encode B={B}: {ms:.3f} ms per call", flush=True)
+    for r in rows[:40]:
+        print(f"  {r['name'][:88]:88s} n={r['launches']:4d} {r['total_ms']:8.3f} ms  roof {r['roof_ms']:7.3f}", flush=True)
+
+
 def bench_attn(B=32):
     """DiT self-attention at the bench shape (L = 467, 8 heads x 72), fp16 operands"""
     L, H = 467, 576
@@ -424,4 +443,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
