@@ -198,10 +198,11 @@ constexpr int FR_THREADS = 1024;  // 16 waves: 4 per SIMD hide the per-tile soft
 // (round 4: scores in the log2 domain (q pre-scaled), exp2 straight to v_exp_f32, masking only in the last key tile,
 // the running-output rescale skipped when no query's max moved)
 
-template <int PREC>
+template <int PREC, bool BIAS>
 __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float* __restrict__ qkv, float* __restrict__ O,
                                                              u16* __restrict__ Op, int L, int Lp, int H, int nh,
-                                                             int dh, float scale) {
+                                                             int dh, float scale, const float* __restrict__ bias,
+                                                             int bld) {
   __shared__ __attribute__((aligned(16))) u16 Ks[FR_MAXL * FR_KS];
   __shared__ __attribute__((aligned(16))) u16 Vt[FR_MAXDH * (FR_MAXL + 8)];
   const int VS = Lp + 8;  // V^T row stride: (VS * 2 / 4) mod 64 = 4 * odd -> conflict-free ds_read_b64
@@ -301,6 +302,16 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
           s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
         }
       }
+      if constexpr (BIAS) {  // additive score bias [head][query][key] (T5's relative positions), into the log2 domain too
+        const float* br = bias + ((int64_t)h * bld + min(q0 + cq, L - 1)) * bld;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + 16 * kb + 4 * g + r;
+            s[kb][r] += br[min(key, L - 1)] * 1.44269504088896341f;
+          }
+      }
       if (k0 + FA_KT > L) {  // (wave-uniform) only the last tile has keys >= L
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
@@ -384,32 +395,32 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
 }
 
 // qkv: (B, L, 3H) fp32 rows [q | k | v], head h at columns h*dh; O: (B, L, H) fp32
-int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s, void* o_plane) {
+int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s, void* o_plane,
+                    const float* bias, int bld, float scale_in) {
   if (!qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
   const int dh = H / nh;
   if (dh > 72 || dh % 4 || H % 4) return set_error(ALCM_E_INVALID, "flash_attention: head dim must be <= 72, % 4");
   if (prec != PREC_F16 && prec != PREC_BF16) return set_error(ALCM_E_INVALID, "flash_attention: F16 or BF16 only");
   if (((uintptr_t)qkv) & 15) return set_error(ALCM_E_INVALID, "flash_attention: qkv must be 16-byte aligned");
-  const float scale = 1.0f / std::sqrt((float)dh);
+  const float scale = scale_in > 0.f ? scale_in : 1.0f / std::sqrt((float)dh);
+  if (bias && bld < L) return set_error(ALCM_E_INVALID, "flash_attention: bias pitch < L");
   const int Lp = (L + FA_KT - 1) / FA_KT * FA_KT;
   if (Lp <= FR_MAXL && dh <= FR_MAXDH && !knobs().attn_tiled && (int64_t)B * nh < (1ll << 31)) {
     void* tok = prof_start(s);
     const dim3 grid((unsigned)(B * nh));
-    if (prec == PREC_F16)
-      hipLaunchKernelGGL(flash_attn_res_kernel<PREC_F16>, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh, dh,
-                         scale);
-    else
-      hipLaunchKernelGGL(flash_attn_res_kernel<PREC_BF16>, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh,
-                         dh, scale);
+    auto kern = prec == PREC_F16 ? (bias ? flash_attn_res_kernel<PREC_F16, true> : flash_attn_res_kernel<PREC_F16, false>)
+                                 : (bias ? flash_attn_res_kernel<PREC_BF16, true> : flash_attn_res_kernel<PREC_BF16, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh, dh, scale, bias, bld);
     if (tok) {
       char name[64];
-      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d>", prec);
+      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d, %s>", prec, bias ? "true" : "false");
       const double z = (double)B * nh;
       prof_stop(tok, s, name, z * 4.0 * L * (double)L * dh, (double)B * L * (3.0 * H + H) * 4.0);
     }
     ALCM_HIP(hipGetLastError());
     return 0;
   }
+  if (bias || scale_in > 0.f) return set_error(ALCM_E_INVALID, "flash_attention: score bias / scale only for L <= 512");
   const int64_t nwg = (int64_t)((L + FA_Q - 1) / FA_Q) * B * nh;
   if (nwg >= (1ll << 31)) return set_error(ALCM_E_INVALID, "flash_attention: problem too large");
   const dim3 grid((unsigned)nwg);

@@ -1783,12 +1783,19 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   // an in-kernel conversion ran the text towers at 0.05 of the MFMA peak (profiles/r3z, bench components)
   const bool planes = (pl == PREC_F16 || pl == PREC_BF16) && H % 64 == 0 && D % 64 == 0 && TI % 64 == 0 &&
                       X.b_inter % 64 == 0 && X.t_ff % 64 == 0;
+  // attention of both towers in the fused kernel (ALCM_TEXT_FLASH=0: score GEMM + softmax + PV GEMM)
+  const bool tflash = planes && knobs().text_flash && L <= 512 && H / X.b_heads <= 72 && X.t_dkv <= 72 &&
+                      (H / X.b_heads) % 4 == 0 && X.t_dkv % 4 == 0;
   for (const BertLayerW& Ly : X.bl) {
     if (planes) {
       ALCM_TRY(to_planes(w.x, w.pl, R, H, H, pl, s));
       ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.qkv, w.qkv, nullptr, 0));
-      ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
-      ALCM_TRY(to_planes(w.O, w.pl, R, H, H, pl, s));
+      if (tflash) {  // fused attention writing the out-projection's operand plane (L = 77: resident K / V)
+        ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, H, X.b_heads, pl, s, w.pl));
+      } else {
+        ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
+        ALCM_TRY(to_planes(w.O, w.pl, R, H, H, pl, s));
+      }
       ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.ao, w.tmp, w.x, 0));
       ALCM_TRY(layer_norm_plane(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, w.pl, pl, s));
       ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, nullptr, 0, w.x, H, s));
@@ -1831,8 +1838,12 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
     if (planes) {
       ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln0, w.pl, pl, s));
       ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.qkv, w.qkv, nullptr, 0));
-      ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
-      ALCM_TRY(to_planes(w.O, w.pl, R, TI, TI, pl, s));
+      if (tflash) {  // unscaled scores + the relative-position bias inside the fused kernel
+        ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, TI, X.t_heads, pl, s, w.pl, X.t_bias, X.max_len, 1.0f));
+      } else {
+        ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
+        ALCM_TRY(to_planes(w.O, w.pl, R, TI, TI, pl, s));
+      }
       ALCM_TRY(plane_lin(s, pl, R, w.pl, TI, Bk.o, w.x, w.x, 0));
       ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln1, w.pl, pl, s));
       ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.wi, w.wi, nullptr, 0));
