@@ -37,6 +37,7 @@ struct WConvDev {
   int n_major;          // workgroup order: 0 = M-tile major (N tiles of an M tile adjacent), 1 = N-tile major
   int ostride, ooff, orows;  // wconv2 output row of input row t: t * ostride + ooff of orows per batch
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
+  int out_act;          // wconv2: activation of acc + bias (ALCM_ACT_*, 0 = none)
 };
 
 
@@ -118,7 +119,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     for (int j = 0; j < BPW; ++j) {
       const int n = 8 * (wave + 4 * j) + (lane >> 3);
       const int ls = (lane & 7) ^ (n & 7);
-      bsrc[j] = P.w + (int64_t)(col0 + n) * P.kpad + ls * 8;
+      bsrc[j] = P.w + (int64_t)min(col0 + n, P.N - 1) * P.kpad + ls * 8;  // (a partial last N tile: rows clamped,
+                                                                          // their columns never stored)
     }
     auto stage_w = [&](int c) {
 #pragma unroll
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int idx = tid + (e0 + e) * 256;
         const int m = idx / cq, n = (idx - m * cq) * 4;
         const int t = min(r0 + m, P.T - 1);
-        const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + col0 + n;
+        const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + min(col0 + n, P.N - 4);
         rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
         pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -268,12 +270,16 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       for (int e = 0; e < PH; ++e) {
         const int idx = tid + (e0 + e) * 256;
         const int m = idx / cq, n = (idx - m * cq) * 4;
-        if (r0 + m >= P.T) continue;
+        if (r0 + m >= P.T || col0 + n >= P.N) continue;
         const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
         if (P.bias) {
           const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
           v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+        }
+        if (P.out_act) {  // (opconv's order: act(acc + bias), then residual / scale / accumulate)
+          v.x = alcm_act(v.x, P.out_act); v.y = alcm_act(v.y, P.out_act);
+          v.z = alcm_act(v.z, P.out_act); v.w = alcm_act(v.w, P.out_act);
         }
         v.x = (v.x + rv[e].x) * P.out_scale + pv[e].x;
         v.y = (v.y + rv[e].y) * P.out_scale + pv[e].y;
@@ -664,8 +670,11 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     return 1;
   if (off && !a.geglu_plane && !strided) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  if (a.out_act || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > W2_HALO) return 0;
-  if (a.N % 96) return 0;
+  if ((a.out_act && (a.geglu_plane || strided)) || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > W2_HALO)
+    return 0;
+  // N % 96: whole tiles; else (N % 4, not strided / GEGLU) 128 x 192 tiles with a partial last one (the T5 wi, N = 5632)
+  const bool ragged = a.N % 96 != 0;
+  if (ragged && (a.N % 4 || strided || a.geglu_plane)) return 0;
   if (!a.geglu_plane && !strided && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
                                                                                      // 128-row tiles fill the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
@@ -673,15 +682,16 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   if (a.geglu_plane && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
   // wconv2 tile (ALCM_WCONV_TILE): 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
   const int tk = knobs().wconv_tile;
-  const bool t256 = a.N % 96 == 0 && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
+  const bool t256 = !ragged && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
   const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
-  if (a.N % BN2 == 0) {
+  if (a.N % BN2 == 0 || ragged) {
     WConvDev P{};
     P.a = (const u16*)a.a;
     P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
     P.w = wplane; P.kpad = a.kpad; P.N = a.N;
     P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
     P.gplane = (u16*)a.geglu_plane;
+    P.out_act = a.out_act;
     P.ostride = strided ? a.out_stride : 1;
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;
@@ -694,7 +704,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     // re-reads the weights from the Infinity Cache once per M tile, 3 GB counted per launch)
     P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && (tiles_m >= 128 || (a.geglu_plane && tiles_m >= 64)));
     P.tiles_per_batch = (a.T + BM2 - 1) / BM2;
-    P.tiles_n = a.N / BN2;
+    P.tiles_n = (a.N + BN2 - 1) / BN2;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
     if (nwg2 >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40)) return 0;
     P.nwg = (int)nwg2;

@@ -359,6 +359,32 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
         assert rel_l2(y.numpy(), y0.numpy()) < 1e-5, (knob, var)
 
 
+@pytest.mark.parametrize("C,N,T,k,act", [(256, 200, 700, 1, 2), (256, 200, 700, 3, 0), (768, 1000, 300, 1, 2),
+                                          (192, 388, 1300, 3, 1)])
+@pytest.mark.parametrize("prec", [0, 2])
+def test_wconv2_ragged_n_out_act(K, C, N, T, k, act, prec, monkeypatch):
+    """Two-workgroup wide conv with N not a multiple of 96 (a partial last 192-column tile: weight rows clamped, its
+    columns masked; the T5 wi at N = 5632) and an output activation (act(acc + bias), the BERT intermediate GELU) vs
+    F.conv1d and vs opconv_kernel (ALCM_WCONV=0) on the same planes."""
+    from audiolcm_amd import _hip
+    B = 2
+    x = _r((B, T, C), 170)
+    w, bias = _r((N, C, k), 171, 0.7 / np.sqrt(C * k)), _r((N,), 172, 0.05)
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias, padding=(k - 1) // 2).permute(0, 2, 1)
+    ref = {0: ref, 1: F.silu(ref), 2: F.gelu(ref)}[act]
+    pl = K.operand_planes(dev(x), prec)
+    y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, out_act=act).cpu()
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+    monkeypatch.setenv("ALCM_WCONV", "0")
+    _hip.reload_knobs()
+    try:
+        y0 = K.opconv(pl, C, dev(w), dev(bias), 1, prec, out_act=act).cpu()
+    finally:
+        monkeypatch.delenv("ALCM_WCONV")
+        _hip.reload_knobs()
+    assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("C,T,k,dil,grid", [(384, 1100, 7, 3, 0), (384, 1100, 7, 3, 8), (192, 1500, 3, 1, 16),
                                             (768, 600, 11, 5, 8), (576, 467, 9, 1, 0)])
 @pytest.mark.parametrize("prec", [0, 2])
