@@ -198,8 +198,33 @@ constexpr int FR_THREADS = 1024;  // 16 waves: 4 per SIMD hide the per-tile soft
 // (round 4: scores in the log2 domain (q pre-scaled), exp2 straight to v_exp_f32, masking only in the last key tile,
 // the running-output rescale skipped when no query's max moved)
 
-template <int PREC, bool BIAS>
-__global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float* __restrict__ qkv, float* __restrict__ O,
+// qkv element idx as fp32: from fp32 rows, or (QH) from PREC operand rows (the DiT q/k/v projection's plane output)
+template <int PREC, bool QH>
+__device__ __forceinline__ float fa_ld(const void* qkv, int64_t idx) {
+  if constexpr (!QH) {
+    return reinterpret_cast<const float*>(qkv)[idx];
+  } else {
+    const u16 v = reinterpret_cast<const u16*>(qkv)[idx];
+    if constexpr (PREC == PREC_F16) return (float)__builtin_bit_cast(_Float16, v);
+    else return __builtin_bit_cast(float, (uint32_t)v << 16);
+  }
+}
+template <int PREC, bool QH>
+__device__ __forceinline__ float4 fa_ld4(const void* qkv, int64_t idx) {
+  if constexpr (!QH) {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(qkv) + idx);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const u16*>(qkv) + idx);
+    auto cv = [](uint32_t h) -> float {
+      if constexpr (PREC == PREC_F16) return (float)__builtin_bit_cast(_Float16, (u16)h);
+      else return __builtin_bit_cast(float, h << 16);
+    };
+    return make_float4(cv(u.x & 0xffffu), cv(u.x >> 16), cv(u.y & 0xffffu), cv(u.y >> 16));
+  }
+}
+
+template <int PREC, bool BIAS, bool QH>
+__global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const void* __restrict__ qkv, float* __restrict__ O,
                                                              u16* __restrict__ Op, int L, int Lp, int H, int nh,
                                                              int dh, float scale, const float* __restrict__ bias,
                                                              int bld) {
@@ -210,7 +235,7 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
   const int g = lane >> 4, cq = lane & 15;
   const int z = blockIdx.x, b = z / nh, h = z - b * nh;
   const int64_t rs = 3 * (int64_t)H;
-  const float* base = qkv + (int64_t)b * L * rs + h * dh;
+  const int64_t base = (int64_t)b * L * rs + h * dh;  // element offset of this (clip, head)
 
   // stage K [key][dim] (dims >= dh and keys >= L zero) and V^T [dim][key] (keys >= L zero); 8 items per thread
   // per round so 16 float4 loads are in flight per lane (the staging phase is HBM-latency bound otherwise)
@@ -225,9 +250,9 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
       kv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < nitem && kr < L && d4 < dh) {
-        const float* r = base + (int64_t)kr * rs + d4;
-        kv[u] = *reinterpret_cast<const float4*>(r + H);
-        vv[u] = *reinterpret_cast<const float4*>(r + 2 * H);
+        const int64_t r = base + (int64_t)kr * rs + d4;
+        kv[u] = fa_ld4<PREC, QH>(qkv, r + H);
+        vv[u] = fa_ld4<PREC, QH>(qkv, r + 2 * H);
       }
     }
 #pragma unroll
@@ -259,14 +284,14 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
     {
       const int q = q0 + cq;
       const bool qok = q < L;
-      const float* qr = base + (int64_t)(qok ? q : 0) * rs;
+      const int64_t qr = base + (int64_t)(qok ? q : 0) * rs;
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) {
         u16 e[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int d = 32 * ks + 8 * g + j;
-          const float v = qr[d < dh ? d : 0];
+          const float v = fa_ld<PREC, QH>(qkv, qr + (d < dh ? d : 0));
           e[j] = fa_cvt<PREC>((qok && d < dh) ? v * qs : 0.f);
         }
         qf[ks] = __builtin_bit_cast(bf16x8, e);
@@ -396,7 +421,30 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const float*
 
 // qkv: (B, L, 3H) fp32 rows [q | k | v], head h at columns h*dh; O: (B, L, H) fp32
 int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s, void* o_plane,
-                    const float* bias, int bld, float scale_in) {
+                    const float* bias, int bld, float scale_in, const void* qkv_plane) {
+  if (qkv_plane) {  // q / k / v as PREC operand rows: the resident-K/V kernel only
+    const int Lp = (L + FA_KT - 1) / FA_KT * FA_KT;
+    const int dh = nh > 0 ? H / nh : 0;
+    if (qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh || dh > FR_MAXDH || dh % 4 || Lp > FR_MAXL ||
+        (prec != PREC_F16 && prec != PREC_BF16) || (((uintptr_t)qkv_plane) & 7) || knobs().attn_tiled ||
+        (bias && bld < L))
+      return set_error(ALCM_E_INVALID, "flash_attention: bad plane-input arguments");
+    const float scale = scale_in > 0.f ? scale_in : 1.0f / std::sqrt((float)dh);
+    void* tok = prof_start(s);
+    auto kern = prec == PREC_F16
+                    ? (bias ? flash_attn_res_kernel<PREC_F16, true, true> : flash_attn_res_kernel<PREC_F16, false, true>)
+                    : (bias ? flash_attn_res_kernel<PREC_BF16, true, true> : flash_attn_res_kernel<PREC_BF16, false, true>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(B * nh)), dim3(FR_THREADS), 0, s, qkv_plane, O, (u16*)o_plane, L, Lp, H, nh,
+                       dh, scale, bias, bld);
+    if (tok) {
+      char name[80];
+      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d, %s, true>", prec, bias ? "true" : "false");
+      const double z = (double)B * nh;
+      prof_stop(tok, s, name, z * 4.0 * L * (double)L * dh, (double)B * L * (3.0 * H * 2.0 + H * 2.0));
+    }
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
   if (!qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh) return set_error(ALCM_E_INVALID, "flash_attention: bad args");
   const int dh = H / nh;
   if (dh > 72 || dh % 4 || H % 4) return set_error(ALCM_E_INVALID, "flash_attention: head dim must be <= 72, % 4");
@@ -408,12 +456,13 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
   if (Lp <= FR_MAXL && dh <= FR_MAXDH && !knobs().attn_tiled && (int64_t)B * nh < (1ll << 31)) {
     void* tok = prof_start(s);
     const dim3 grid((unsigned)(B * nh));
-    auto kern = prec == PREC_F16 ? (bias ? flash_attn_res_kernel<PREC_F16, true> : flash_attn_res_kernel<PREC_F16, false>)
-                                 : (bias ? flash_attn_res_kernel<PREC_BF16, true> : flash_attn_res_kernel<PREC_BF16, false>);
+    auto kern = prec == PREC_F16
+                    ? (bias ? flash_attn_res_kernel<PREC_F16, true, false> : flash_attn_res_kernel<PREC_F16, false, false>)
+                    : (bias ? flash_attn_res_kernel<PREC_BF16, true, false> : flash_attn_res_kernel<PREC_BF16, false, false>);
     hipLaunchKernelGGL(kern, grid, dim3(FR_THREADS), 0, s, qkv, O, (u16*)o_plane, L, Lp, H, nh, dh, scale, bias, bld);
     if (tok) {
       char name[64];
-      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d, %s>", prec, bias ? "true" : "false");
+      std::snprintf(name, sizeof(name), "alcm::flash_attn_res_kernel<%d, %s, false>", prec, bias ? "true" : "false");
       const double z = (double)B * nh;
       prof_stop(tok, s, name, z * 4.0 * L * (double)L * dh, (double)B * L * (3.0 * H + H) * 4.0);
     }

@@ -65,9 +65,11 @@ int nconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const voi
               hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
 // o_plane != nullptr: write the output as an fp16 / bf16 operand plane [B][L][H] instead of fp32 O
-// bias != nullptr: + bias[(head * bld + query) * bld + key] on the scores (L <= 512); scale > 0 replaces 1/sqrt(dh)
+// bias != nullptr: + bias[(head * bld + query) * bld + key] on the scores (L <= 512); scale > 0 replaces 1/sqrt(dh);
+// qkv_plane != nullptr (then qkv == nullptr): q / k / v rows as PREC operand elements (L <= 512)
 int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int prec, hipStream_t s,
-                    void* o_plane = nullptr, const float* bias = nullptr, int bld = 0, float scale = 0.f);
+                    void* o_plane = nullptr, const float* bias = nullptr, int bld = 0, float scale = 0.f,
+                    const void* qkv_plane = nullptr);
 // whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
 bool opconv_act_supported(int prec, int N, int Cp_in);
 int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, double flops, double bytes,
@@ -126,6 +128,7 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
+  int qkv_plane = 1;             // ALCM_QKV_PLANE: DiT q/k/v projection writes an fp16 plane for the attention (0 = fp32)
   int text_flash = 1;            // ALCM_TEXT_FLASH: text-encoder attention in the fused kernel (0 = GEMM + softmax + GEMM)
   int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)
   int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs

@@ -862,8 +862,15 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       g.a = pln; g.B = B; g.T = L; g.C = H; g.Cp = wq.w.cpad; g.ksize = 1; g.dil = 1; g.pad = 0;
       g.w = wq.w.p; g.w_lo_off = wq.w.lo; g.kpad = wq.w.kpad; g.N = wq.w.rows;
       g.bias = wq.b; g.out = w.qkv; g.out_scale = 1.f; g.prec = pff;
+      // q / k / v as an operand plane (attention rounds them to pff anyway): half the bytes written and staged
+      const bool qp = knobs().qkv_plane && wq.w.rows % 4 == 0 && L <= 512;
+      if (qp) {
+        g.out = nullptr;
+        g.out_plane = w.qkv;
+      }
       ALCM_TRY(opconv(g, s));
-      ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, H, D.heads, pff, s, opl));
+      if (qp) ALCM_TRY(flash_attention(nullptr, nullptr, B, L, H, D.heads, pff, s, opl, nullptr, 0, 0.f, w.qkv));
+      else ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, H, D.heads, pff, s, opl));
       std::memset(&g, 0, sizeof(g));
       g.a = opl; g.B = B; g.T = L; g.C = H; g.Cp = wo.w.cpad; g.ksize = 1; g.dil = 1; g.pad = 0;
       g.w = wo.w.p; g.w_lo_off = wo.w.lo; g.kpad = wo.w.kpad; g.N = wo.w.rows;

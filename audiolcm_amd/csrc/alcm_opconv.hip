@@ -680,7 +680,7 @@ bool opconv_act_supported(int prec, int N, int Cp_in) {
 
 int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const bool act = a.act_plane != nullptr;
-  if (!a.a || !a.w || (!a.out && !act && !a.geglu_plane) || a.B <= 0 || a.T <= 0 || a.N <= 0 || a.ksize <= 0 || a.dil <= 0)
+  if (!a.a || !a.w || (!a.out && !act && !a.geglu_plane && !a.out_plane) || a.B <= 0 || a.T <= 0 || a.N <= 0 || a.ksize <= 0 || a.dil <= 0)
     return set_error(ALCM_E_INVALID, "opconv: bad arguments");
   if (a.Cp <= 0 || a.Cp % 32) return set_error(ALCM_E_INVALID, "opconv: Cp must be a positive multiple of 32");
   if ((a.ksize - 1) * a.dil > OC_HALO) return set_error(ALCM_E_INVALID, "opconv: receptive field too large");
@@ -738,6 +738,14 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   const double bytes = M * a.Cp * 2.0 * npa + (double)a.N * a.kpad * 2.0 * npb +
                        M * a.N * 4.0 * ((a.out ? 1 : 0) + (a.res ? 1 : 0) + (a.accumulate ? 1 : 0)) +
                        (act ? M * round_up(a.N, 32) * 2.0 * npa : 0.0);
+  if (a.out_plane) {  // only the wide-layer kernel has the plane-output epilogue
+    if (a.res || a.accumulate || a.out_act || act || a.geglu_plane || strided || a.out ||
+        (a.prec != PREC_F16 && a.prec != PREC_BF16) || (((uintptr_t)a.out_plane) & 7) || !wconv_try(a, P.w, flops, bytes, s))
+      return set_error(ALCM_E_INVALID, "opconv: plane output needs F16/BF16, N % 4 == 0, Cp % 64 == 0, out == NULL "
+                                       "and no res/accumulate/act/GEGLU/strided output");
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
   if (a.geglu_plane) {  // only the wide-layer kernel has the GEGLU epilogue
     if (!wconv_try(a, P.w, flops, bytes, s))
       return set_error(ALCM_E_INVALID, "opconv: GEGLU plane epilogue needs F16/BF16, N % 128 == 0, Cp % 64 == 0, "

@@ -38,6 +38,7 @@ struct WConvDev {
   int ostride, ooff, orows;  // wconv2 output row of input row t: t * ostride + ooff of orows per batch
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int out_act;          // wconv2: activation of acc + bias (ALCM_ACT_*, 0 = none)
+  u16* oplane;          // wconv2: conv + bias as an operand plane [B][T][N] (PREC) instead of the fp32 output
 };
 
 
@@ -276,6 +277,11 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         if (P.bias) {
           const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
           v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
+        }
+        if (P.oplane) {  // plane output (no residual / accumulate / act): 4 rounded values, one 8-B store
+          op_store2<PREC>(P.oplane + go, 0, f32x2{v.x, v.y});
+          op_store2<PREC>(P.oplane + go + 2, 0, f32x2{v.z, v.w});
+          continue;
         }
         if (P.out_act) {  // (opconv's order: act(acc + bias), then residual / scale / accumulate)
           v.x = alcm_act(v.x, P.out_act); v.y = alcm_act(v.y, P.out_act);
@@ -668,14 +674,14 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || (full && fills)) &&
       wconv3_try(a, wplane, flops, bytes, s))
     return 1;
-  if (off && !a.geglu_plane && !strided) return 0;
+  if (off && !a.geglu_plane && !strided && !a.out_plane) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if ((a.out_act && (a.geglu_plane || strided)) || a.Cp % 64 || a.ksize < 1 || (a.ksize - 1) * a.dil > W2_HALO)
     return 0;
   // N % 96: whole tiles; else (N % 4, not strided / GEGLU) 128 x 192 tiles with a partial last one (the T5 wi, N = 5632)
   const bool ragged = a.N % 96 != 0;
   if (ragged && (a.N % 4 || strided || a.geglu_plane)) return 0;
-  if (!a.geglu_plane && !strided && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
+  if (!a.geglu_plane && !strided && !a.out_plane && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
                                                                                      // 128-row tiles fill the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
@@ -692,6 +698,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
     P.gplane = (u16*)a.geglu_plane;
     P.out_act = a.out_act;
+    P.oplane = (u16*)a.out_plane;
     P.ostride = strided ? a.out_stride : 1;
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;

@@ -199,6 +199,11 @@ typedef struct alcm_opconv_args {
    * Needs F16/BF16, N % 192 == 0, Cp % 64 == 0 and no res / accumulate / out_act / act / GEGLU.
    * 0 (the zero-initialised default): same-length conv, out is [B][T][N]. */
   int out_stride, out_offset, out_rows;
+  /* optional operand-plane output: when out_plane != NULL the kernel writes conv + bias as an F16 / BF16 plane
+   * [B][T][N] (the format of `prec`) instead of the fp32 `out` (which may be NULL) — for a consumer that rounds to
+   * that format anyway (the DiT q/k/v projection feeding the fused attention).  Needs the wide-layer kernel
+   * (F16 / BF16, N % 4 == 0, Cp % 64 == 0) and no res / accumulate / out_act / act / GEGLU / strided output. */
+  void* out_plane;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 /* alcm_opconv_dense: the narrow AMPBlock conv of BigVGAN stages 3-5 (vocoder/bigvgan/models.py:72-81, C = N in
