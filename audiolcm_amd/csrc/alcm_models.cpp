@@ -1762,13 +1762,14 @@ static int lin(hipStream_t s, int prec, int R, const float* x, int C, const Conv
 // the same linear on an F16 / BF16 operand plane (alcm_opconv, k = 1: the wide-layer / plane conv kernels): y (R, N) =
 // plane (R, C) W^T (+ bias) (+ res) with out_act; the plane is written by the caller
 static int plane_lin(hipStream_t s, int prec, int R, const u16* plane, int C, const ConvW& w, float* y,
-                     const float* res, int act, int64_t plane_lo = 0) {
+                     const float* res, int act, int64_t plane_lo = 0, void* out_plane = nullptr) {
   if (w.w.cpad != C || w.w.taps != 1) return set_error(ALCM_E_INVALID, "plane_lin: plane width != packed Cin");
   alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
   g.a = plane; g.a_lo_off = plane_lo; g.B = 1; g.T = R; g.C = C; g.Cp = C; g.ksize = 1; g.dil = 1; g.pad = 0;
   g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.N = w.w.rows;
   g.bias = w.b; g.res = res; g.out = y; g.out_act = act; g.out_scale = 1.f; g.prec = prec;
+  g.out_plane = out_plane;  // (then y == nullptr: the result as a PREC plane)
   return opconv(g, s);
 }
 
@@ -1796,10 +1797,11 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   for (const BertLayerW& Ly : X.bl) {
     if (planes) {
       ALCM_TRY(to_planes(w.x, w.pl, R, H, H, pl, s));
-      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.qkv, w.qkv, nullptr, 0));
-      if (tflash) {  // fused attention writing the out-projection's operand plane (L = 77: resident K / V)
-        ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, H, X.b_heads, pl, s, w.pl));
+      if (tflash) {  // q / k / v as a plane, fused attention writing the out-projection's plane (resident K / V)
+        ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.qkv, nullptr, nullptr, 0, 0, w.qkv));
+        ALCM_TRY(flash_attention(nullptr, nullptr, B, L, H, X.b_heads, pl, s, w.pl, nullptr, 0, 0.f, w.qkv));
       } else {
+        ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.qkv, w.qkv, nullptr, 0));
         ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
         ALCM_TRY(to_planes(w.O, w.pl, R, H, H, pl, s));
       }
@@ -1844,10 +1846,12 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   for (const T5BlockW& Bk : X.tb) {
     if (planes) {
       ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln0, w.pl, pl, s));
-      ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.qkv, w.qkv, nullptr, 0));
       if (tflash) {  // unscaled scores + the relative-position bias inside the fused kernel
-        ALCM_TRY(flash_attention(w.qkv, nullptr, B, L, TI, X.t_heads, pl, s, w.pl, X.t_bias, X.max_len, 1.0f));
+        ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.qkv, nullptr, nullptr, 0, 0, w.qkv));
+        ALCM_TRY(flash_attention(nullptr, nullptr, B, L, TI, X.t_heads, pl, s, w.pl, X.t_bias, X.max_len, 1.0f,
+                                 w.qkv));
       } else {
+        ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.qkv, w.qkv, nullptr, 0));
         ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
         ALCM_TRY(to_planes(w.O, w.pl, R, TI, TI, pl, s));
       }
