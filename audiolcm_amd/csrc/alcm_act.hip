@@ -264,6 +264,12 @@ __global__ __launch_bounds__(256, 2) void act_mfma_kernel(const float* __restric
       const _Float16 hi = (_Float16)tv;
       bdn[p][e] = (e & 1) ? (_Float16)(tv - (float)hi) : hi;
     }
+  // samples AM_UPB * 16 .. AM_SS - 1 of each channel row are read by the last down blocks against zero taps but never
+  // written: zero them once (uninitialised LDS could hold NaN bit patterns, and NaN * 0 = NaN)
+  if (q4 == 0) {
+#pragma unroll
+    for (int i = AM_UPB * 16; i < AM_SS; ++i) sw[l16 * AM_SS + i] = 0u;
+  }
   const int cl = c0 + l16;  // this lane's channel in the up products
   const float ear = aexp[cl] * INV_PI, hh = ibeta[cl] * 0.5f;
 

@@ -178,6 +178,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void ampair_kernel(const 
   const int my_n = tbeg < tend ? (tend - tbeg + nslot - 1) / nslot : 0;
   if (my_n == 0) return;
   const int total = my_n * 2 * NS;  // WM 0: weight slices this workgroup streams
+  // the K padding (k >= KS * C) reads up to two rows past the rows act1 writes, against zero weights: start from
+  // zeroed operand rows so those reads are finite (uninitialised LDS could hold NaN bit patterns, NaN * 0 = NaN)
+  for (int i = tid; i < G::A1B / 16; i += NT) reinterpret_cast<uint4*>(abuf)[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
 
   // WM 0: weight slice gs (tile gs / (2 NS), conv (gs / NS) & 1, slice gs % NS) -> ring slot gs % RING; instruction
   // i = wave + NW j covers bytes [1024 i, 1024 i + 1024) of the slot: [plane][row n of 64 B][piece], the 16-B piece
