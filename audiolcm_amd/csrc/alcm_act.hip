@@ -206,11 +206,7 @@ int act_coop(const float* x, void* const* y, int nset, int B, int T, int C, int 
 // UpSample1d's replicate padding) as (v, v) fp16 pairs in LDS [ch][row], 9 up blocks -> 144 samples m = 2 t0 - 5 + i
 // as pairs in LDS [ch][i] (samples outside [0, 2T): DownSample1d's replicate padding, patched in LDS), 4 down blocks
 // -> 4 channels x one output per lane, 8-B plane stores.  No cross-wave sharing: no workgroup barrier.
-constexpr int AM_TT = 64;            // outputs per wave tile
-constexpr int AM_XR = 80;            // staged x rows (77 used)
 constexpr int AM_XS = 84;            // x row stride in pairs: = 20 mod 64 (conflict-free 4-B transposing writes)
-constexpr int AM_SS = 148;           // sample stride in pairs: /4 odd (conflict-free 16-B fragment writes and reads)
-constexpr int AM_UPB = 9;            // up blocks (144 >= 2 AM_TT + 10 samples)
 
 __device__ __forceinline__ float am_sel12(const float (&t)[12], int i) {
   float v = 0.f;
@@ -225,11 +221,24 @@ __device__ __forceinline__ uint32_t am_pair(float v) {  // (v, v) as two fp16
 
 constexpr int AM_STRIP = 8;          // wave tiles per workgroup strip (the tap fragments are built once per strip)
 
-__global__ __launch_bounds__(256, 2) void act_mfma_kernel(const float* __restrict__ x, u16* __restrict__ y, int T,
-                                                          int C, int Cp, const float* __restrict__ aexp,
-                                                          const float* __restrict__ ibeta, const Taps12O f,
-                                                          int strips_t, int tiles_c) {
+// TT outputs per wave tile: 64 (two 59 KB workgroups per CU) or 48 (7 up / 3 down blocks, 51 KB: three per CU)
+template <int TT>
+struct AmGeo {
+  static constexpr int XR = TT + 16;                   // staged x rows
+  static constexpr int UPB = (2 * TT + 10 + 15) / 16;  // up blocks
+  static constexpr int SS = UPB * 16 + 4;              // sample stride in pairs (/4 odd)
+  static constexpr int OCC = TT == 48 ? 3 : 2;
+  static_assert(XR <= AM_XS && (SS / 4) % 2 == 1 && 8 * (UPB - 1) + 15 < XR && TT % 16 == 0, "act_mfma tile");
+};
+
+template <int TT>
+__global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const float* __restrict__ x,
+                                                                          u16* __restrict__ y, int T, int C, int Cp,
+                                                                          const float* __restrict__ aexp,
+                                                                          const float* __restrict__ ibeta,
+                                                                          const Taps12O f, int strips_t, int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_SS = AmGeo<TT>::SS, AM_UPB = AmGeo<TT>::UPB;
   __shared__ __attribute__((aligned(16))) uint32_t xs[4][16 * AM_XS];
   __shared__ __attribute__((aligned(16))) uint32_t ss[4][16 * AM_SS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -366,12 +375,17 @@ bool act_mfma_ok(int C, int Cp, int prec) {
 int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
              const Taps12O& f, hipStream_t s) {
   if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 7)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
-  const int tiles_t = (T + AM_TT - 1) / AM_TT, tiles_c = C / 64;
+  const int TT = knobs().act_tt == 48 ? 48 : 64;
+  const int tiles_t = (T + TT - 1) / TT, tiles_c = C / 64;
   const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
   const int64_t nwg = (int64_t)B * strips_t * tiles_c;
   if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma: too large");
-  hipLaunchKernelGGL(act_mfma_kernel, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp, inv_beta,
-                     f, strips_t, tiles_c);
+  if (TT == 48)
+    hipLaunchKernelGGL(act_mfma_kernel<48>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
+                       inv_beta, f, strips_t, tiles_c);
+  else
+    hipLaunchKernelGGL(act_mfma_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
+                       inv_beta, f, strips_t, tiles_c);
   ALCM_HIP(hipGetLastError());
   return 0;
 }
