@@ -221,7 +221,9 @@ __device__ __forceinline__ uint32_t am_pair(float v) {  // (v, v) as two fp16
 
 constexpr int AM_STRIP = 8;          // wave tiles per workgroup strip (the tap fragments are built once per strip)
 
-// TT outputs per wave tile: 64 (two 59 KB workgroups per CU) or 48 (7 up / 3 down blocks, 51 KB: three per CU)
+// TT outputs per wave tile: 64 (two 59 KB workgroups per CU).  A 48-output tile (7 up / 3 down blocks, 51 KB: three
+// workgroups per CU) measured the same (8.92 vs 8.94 ms/step over the 270 launches, profiles/r4z): occupancy is not
+// what bounds this kernel
 template <int TT>
 struct AmGeo {
   static constexpr int XR = TT + 16;                   // staged x rows
@@ -375,17 +377,13 @@ bool act_mfma_ok(int C, int Cp, int prec) {
 int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
              const Taps12O& f, hipStream_t s) {
   if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 7)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
-  const int TT = knobs().act_tt == 48 ? 48 : 64;
+  constexpr int TT = 64;
   const int tiles_t = (T + TT - 1) / TT, tiles_c = C / 64;
   const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
   const int64_t nwg = (int64_t)B * strips_t * tiles_c;
   if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma: too large");
-  if (TT == 48)
-    hipLaunchKernelGGL(act_mfma_kernel<48>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
-                       inv_beta, f, strips_t, tiles_c);
-  else
-    hipLaunchKernelGGL(act_mfma_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
-                       inv_beta, f, strips_t, tiles_c);
+  hipLaunchKernelGGL(act_mfma_kernel<TT>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
+                     inv_beta, f, strips_t, tiles_c);
   ALCM_HIP(hipGetLastError());
   return 0;
 }

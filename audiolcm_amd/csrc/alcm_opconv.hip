@@ -145,8 +145,7 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
     ALCM_TRY(act_mfma(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
     if (tok) {
       const double e = (double)B * T;
-      prof_stop(tok, s, knobs().act_tt == 48 ? "alcm::act_mfma_kernel<48>" : "alcm::act_mfma_kernel<64>",
-                2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp));
+      prof_stop(tok, s, "alcm::act_mfma_kernel<64>", 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp));
     }
     return 0;
   }
