@@ -243,6 +243,10 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_SS = AmGeo<TT>::SS, AM_UPB = AmGeo<TT>::UPB;
   __shared__ __attribute__((aligned(16))) uint32_t xs[4][16 * AM_XS];
   __shared__ __attribute__((aligned(16))) uint32_t ss[4][16 * AM_SS];
+  // the workgroup's output tile [TT rows][64 channels] (row stride 72 halves), written out as whole 128-B row segments
+  // (each wave's own 32-B pieces of 16 rows left partial lines for the L2 to merge: 1.7x the plane bytes in PMC)
+  constexpr int OS = 72;
+  __shared__ __attribute__((aligned(16))) u16 ob[AM_TT * OS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q4 = lane >> 4, l16 = lane & 15;
   int bid = blockIdx.x;
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
     }
   };
   load_x(tile0 * AM_TT);
-  u16* yb = y + (int64_t)b * T * Cp + c0 + 4 * q4;
+  u16* const yb = y + (int64_t)b * T * Cp + ct * 64;
   for (int tl = 0; tl < ntile; ++tl) {
     const int t0 = (tile0 + tl) * AM_TT;
     // (v, v) fp16 pairs at xw[c * XS + r]
@@ -356,14 +360,20 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
         const f16x8 a = *reinterpret_cast<const f16x8*>(sw + l16 * AM_SS + 32 * d + 16 * p + 4 * q4);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bdn[p], acc, 0, 0, 0);
       }
-      const int j = t0 + 16 * d + l16;
-      if (j < T) {
-        uint2 w;
-        w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
-        w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
-        *reinterpret_cast<uint2*>(yb + (int64_t)j * Cp) = w;
-      }
+      uint2 w;
+      w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
+      w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
+      *reinterpret_cast<uint2*>(ob + (16 * d + l16) * OS + wave * 16 + 4 * q4) = w;
     }
+    __syncthreads();  // every wave's 16 channels of the tile staged
+#pragma unroll
+    for (int k = 0; k < AM_TT * 8 / 256; ++k) {
+      const int e = tid + 256 * k, r = e >> 3, sg = e & 7;
+      if (t0 + r < T)
+        *reinterpret_cast<uint4*>(yb + (int64_t)(t0 + r) * Cp + sg * 8) =
+            *reinterpret_cast<const uint4*>(ob + r * OS + sg * 8);
+    }
+    __syncthreads();  // the staged tile read out before the next tile's down blocks overwrite it
     // the next tile's x pairs overwrite xw only after this tile's up reads retired (same wave, in order)
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -376,7 +386,7 @@ bool act_mfma_ok(int C, int Cp, int prec) {
 
 int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
              const Taps12O& f, hipStream_t s) {
-  if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 7)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
+  if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 15)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
   constexpr int TT = 64;
   const int tiles_t = (T + TT - 1) / TT, tiles_c = C / 64;
   const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;

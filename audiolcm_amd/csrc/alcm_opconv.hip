@@ -140,7 +140,7 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   }
   const int64_t y_lo = (int64_t)B * T * Cp;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-  if (act_mfma_ok(C, Cp, prec)) {  // both FIRs on MFMA (alcm_act.hip): the wide stages under the mixed policy
+  if (act_mfma_ok(C, Cp, prec) && !(((uintptr_t)x) & 15) && !(((uintptr_t)y) & 15)) {  // both FIRs on MFMA (alcm_act.hip): the wide stages under the mixed policy
     void* tok = prof_start(s);
     ALCM_TRY(act_mfma(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
     if (tok) {
