@@ -241,7 +241,10 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
                                                                           const Taps12O f, int strips_t, int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
   constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_SS = AmGeo<TT>::SS, AM_UPB = AmGeo<TT>::UPB;
-  __shared__ __attribute__((aligned(16))) uint32_t xs[4][16 * AM_XS];
+  // per wave [16 ch][XS rows] of (v, v) pairs; waves 4 pairs apart (= 4 mod 64 banks: the cooperative writes below
+  // are conflict-free)
+  constexpr int XWS = 16 * AM_XS + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t xs[4 * XWS];
   __shared__ __attribute__((aligned(16))) uint32_t ss[4][16 * AM_SS];
   // the workgroup's output tile [TT rows][64 channels] (row stride 72 halves), written out as whole 128-B row segments
   // (each wave's own 32-B pieces of 16 rows left partial lines for the L2 to merge: 1.7x the plane bytes in PMC)
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   const int b = bid / strips_t;
   const int c0 = ct * 64 + wave * 16;
   const int tile0 = st * AM_STRIP, ntile = min(AM_STRIP, (T + AM_TT - 1) / AM_TT - tile0);
-  uint32_t* const xw = xs[wave];
+  uint32_t* const xw = xs + wave * XWS;
   uint32_t* const sw = ss[wave];
 
   // tap fragments, once per strip: up A[q = l16][k = 8 q4 + e] = tap_(e&1)[ku], ku = q - 2 r' + 10, r' = 4 q4 + e / 2
@@ -288,14 +291,15 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   const int cl = c0 + l16;  // this lane's channel in the up products
   const float ear = aexp[cl] * INV_PI, hh = ibeta[cl] * 0.5f;
 
-  // x rows t0 - 5 + r (clamped), channels c0 .. c0 + 15: lane = (row, channel quad); the next tile's rows are loaded
-  // into registers while this tile computes
-  const float* xb = x + (int64_t)b * T * C + c0 + (lane & 3) * 4;
+  // x rows t0 - 5 + r (clamped) of the workgroup's 64 channels, loaded cooperatively as whole 256-B row segments: wave
+  // w's instruction it covers rows 16 it + 4 w .. + 3, lane = (row, 16-B piece); each piece belongs to the wave
+  // owning its 16 channels.  The next tile's rows are loaded into registers while this tile computes
+  const float* xb = x + (int64_t)b * T * C + ct * 64 + (lane & 15) * 4;
   float4 xv[AM_XR / 16];
   auto load_x = [&](int t0) {
 #pragma unroll
     for (int it = 0; it < AM_XR / 16; ++it) {
-      const int t = min(max(t0 - 5 + it * 16 + (lane >> 2), 0), T - 1);
+      const int t = min(max(t0 - 5 + it * 16 + wave * 4 + (lane >> 4), 0), T - 1);
       xv[it] = *reinterpret_cast<const float4*>(xb + (int64_t)t * C);
     }
   };
@@ -303,19 +307,22 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   u16* const yb = y + (int64_t)b * T * Cp + ct * 64;
   for (int tl = 0; tl < ntile; ++tl) {
     const int t0 = (tile0 + tl) * AM_TT;
-    // (v, v) fp16 pairs at xw[c * XS + r]
-#pragma unroll
-    for (int it = 0; it < AM_XR / 16; ++it) {
-      const int r = it * 16 + (lane >> 2);
+    // (v, v) fp16 pairs at xw'[c * XS + r] of the owning wave w'
+    {
+      uint32_t* const xo = xs + ((lane & 15) >> 2) * XWS;
       const int c = (lane & 3) * 4;
-      xw[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
-      xw[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
-      xw[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
-      xw[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+#pragma unroll
+      for (int it = 0; it < AM_XR / 16; ++it) {
+        const int r = it * 16 + wave * 4 + (lane >> 4);
+        xo[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
+        xo[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
+        xo[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
+        xo[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+      }
     }
     if (tl + 1 < ntile) load_x(t0 + AM_TT);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's x pairs are in LDS (the prefetch stays in flight)
-    __builtin_amdgcn_wave_barrier();
+    // every wave's x pairs staged: LDS-only wait (a __syncthreads fence would also wait for the prefetch)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
     // up blocks: samples i = 16 bk + 4 q4 + r of channel l16 -> SnakeBeta (fp32) -> (s, s) pairs at sw[l16 SS + i]
 #pragma unroll
@@ -365,7 +372,7 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
       w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
       *reinterpret_cast<uint2*>(ob + (16 * d + l16) * OS + wave * 16 + 4 * q4) = w;
     }
-    __syncthreads();  // every wave's 16 channels of the tile staged
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's 16 channels of the tile staged
 #pragma unroll
     for (int k = 0; k < AM_TT * 8 / 256; ++k) {
       const int e = tid + 256 * k, r = e >> 3, sg = e & 7;
@@ -373,7 +380,9 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
         *reinterpret_cast<uint4*>(yb + (int64_t)(t0 + r) * Cp + sg * 8) =
             *reinterpret_cast<const uint4*>(ob + r * OS + sg * 8);
     }
-    __syncthreads();  // the staged tile read out before the next tile's down blocks overwrite it
+    // the staged tile and the x pairs read out before the next tile overwrites them (LDS only: the stores and the
+    // prefetch stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     // the next tile's x pairs overwrite xw only after this tile's up reads retired (same wave, in order)
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
