@@ -128,7 +128,6 @@ struct Knobs {
                                  // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
-  int act_xcoop = 1;             // ALCM_ACT_XCOOP: act_mfma x window as whole-row cooperative loads (0: per-wave pieces)
   int qkv_plane = 1;             // ALCM_QKV_PLANE: DiT q/k/v projection writes an fp16 plane for the attention (0 = fp32)
   int text_flash = 1;            // ALCM_TEXT_FLASH: text-encoder attention in the fused kernel (0 = GEMM + softmax + GEMM)
   int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)

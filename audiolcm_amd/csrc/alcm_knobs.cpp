@@ -50,7 +50,6 @@ static Knobs read_knobs() {
   k.act3 = env_int("ALCM_ACT3", 1);
   k.text_flash = env_int("ALCM_TEXT_FLASH", 1);
   k.qkv_plane = env_int("ALCM_QKV_PLANE", 1);
-  k.act_xcoop = env_int("ALCM_ACT_XCOOP", 1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
   k.ampair = env_int("ALCM_AMPAIR", 0);  // opt-in until it beats the unfused chain
   k.ampair_grid = env_int("ALCM_AMPAIR_GRID", 0);
