@@ -53,17 +53,12 @@ struct TConvDev {
   int stagger;        // tconv2: s_sleep(127) count before the second half of a persistent grid starts
 };
 
-// staged fp32 row stride (floats): NS + 4, except at NS = 24, where the fused Activation1d's 12-row runs of 12 channel
-// pairs would read the staged tile 2-way bank-conflicted (run offset 12 * 28 = 16 banks); 34 puts consecutive runs 24
-// banks apart, conflict-free for a whole wave
-constexpr int tc_ots(int NS) { return NS == 24 ? 34 : NS + 4; }
-
 __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
 }
 
 // conv tile epilogue shared by the resident- and streamed-weight kernels: v = acc + bias staged in LDS (`ot`, row
-// stride tc_ots(NS) floats; the caller's barrier retired every K-loop read of that region), + residual (rv: the tile
+// stride NS + 4 floats; the caller's barrier retired every K-loop read of that region), + residual (rv: the tile
 // rows' residual, prefetched as float4 element e = tid + i * NT), fp32 state / accumulated output of the owned rows,
 // Activation1d of the owned rows into the next conv's planes
 template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, bool RES, bool OUTW, bool ACC,
@@ -71,7 +66,7 @@ template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, boo
 __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const float (&bias_r)[TN],
                                           const float4 (&rv)[PRE ? NRES : 1], float* ot, int wr0, int t0, int e0, int E,
                                           int b, int n0, const TConvDev& P) {
-  constexpr int OTS = tc_ots(NS);
+  constexpr int OTS = NS + 4;
   const int tid = threadIdx.x, lane = tid & 63, q4 = lane >> 4, l16 = lane & 15;
   // v = conv + bias -> LDS
 #pragma unroll
@@ -131,7 +126,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
   constexpr int RS = RSS * 16;
   constexpr int WRMAX = BM + 64;
   constexpr int WIN_INSTR = (WRMAX * RSS + 63) / 64;    // window DMA instructions per tile (64 slots each)
-  constexpr int OTS = tc_ots(NS);                       // staged fp32 row stride (floats)
+  constexpr int OTS = NS + 4;                           // staged fp32 row stride (floats)
   constexpr int STAGE = BM * OTS * 4;
   constexpr int WINB = WIN_INSTR * 1024;
   constexpr int REGION = STAGE > WINB ? STAGE : WINB;   // window, then (after the K loop) the staged tile
@@ -287,7 +282,7 @@ __global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TC
   constexpr int RING = 4;
   constexpr int WINB = WPW * 4 * 1024;
   constexpr int RINGB = RING * SLOT;
-  constexpr int OTS = tc_ots(NS);
+  constexpr int OTS = NS + 4;
   constexpr int STAGE = BM * OTS * 4;
   constexpr int REGION = (STAGE > WINB + RINGB ? STAGE : WINB + RINGB);
   constexpr int SMEM = REGION + 1024 * 4;               // + one scratch KB per wave for padding DMA instructions
