@@ -98,6 +98,8 @@ bool sgemm_planes_ok(int K, int N, int kpad);
 int sgemm_planes(const unsigned short* a, int64_t a_lo, int M, int K, const unsigned short* w, int64_t w_lo, int kpad,
                  int N, const float* bias, const float* res, int64_t ldr, float* out, int64_t ldo, float out_scale,
                  hipStream_t s);
+// single-plane 1x1 conv / linear (alcm_sgemm.hip, ALCM_LIN1); 1 when it launched, 0 when not eligible
+int lin_plane_try(const alcm_opconv_args& a, const unsigned short* wplane, double flops, double bytes, hipStream_t s);
 int split_planes(const float* x, int64_t rows, int C, int T, const float* scale, const float* shift,
                  unsigned short* y, hipStream_t s);
 
@@ -132,6 +134,8 @@ struct Knobs {
   int text_flash = 1;            // ALCM_TEXT_FLASH: text-encoder attention in the fused kernel (0 = GEMM + softmax + GEMM)
   int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)
   int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs
+  int lin1 = 1;                  // ALCM_LIN1: single-plane 1x1 convs on lin_plane_kernel (1: 32-deep 4-stage ring, 2: 64-deep
+                                 // double-buffered), 0 = wconv2
   int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
   bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)

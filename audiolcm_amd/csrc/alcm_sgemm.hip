@@ -16,6 +16,7 @@
 
 #include "alcm_common.h"
 #include "alcm_internal.h"
+#include "alcm_actepi.h"  // op_store2 / f32x2 (plane output)
 
 namespace alcm {
 
@@ -35,6 +36,7 @@ struct SGemmDev {
   int64_t ldo;
   float out_scale;
   int tiles_n, nwg;
+  u16* oplane;       // single-plane kernel: acc + bias as a PREC operand plane [M][ldo] instead of out
 };
 
 constexpr int SG_BM = 128, SG_BN = 192;
@@ -49,20 +51,27 @@ __device__ __forceinline__ void sg_glds16(const void* src, char* lds) {
 // against 64-deep stages (whole 128-B row segments) at one per CU, per step 1.69 vs 2.23 / 2.12 ms over the 120
 // launches (DiT proj_in / proj_out 0.94 vs 1.26 / 1.21; bit-identical; +0.6 % end to end, profiles/r4m) — the DiT
 // shape's 351 tiles then run in one round instead of 1.4, and the co-resident workgroup hides the DMA waits
-template <int KD, int NST, int OCC>
-__global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P) {
+//
+// NPL = 1 (lin_plane_kernel): the same structure on ONE operand plane (PREC f16 / bf16, one MFMA per fragment pair) for
+// the 1x1 convs / linears of the single-plane policies (DiT q,k,v and to_out, text-encoder linears): wconv2 stages its
+// input window once per 64-channel chunk, which at k = 1 is every step, so each step waited out a full window DMA
+// (68 us per DiT q,k,v launch against a 12 us MFMA floor); here 20 KB stages in a 4-deep ring keep three in flight.
+// Same 32-deep slice order as wconv2, so the results are bit-identical to it.
+template <int KD, int NST, int OCC, int NPL, int PREC>
+__device__ __forceinline__ void sg_body(const SGemmDev& P) {
   constexpr int TM = 4, TN = 6;
-  constexpr int RB = KD * 2;              // LDS row bytes
-  constexpr int AB = SG_BM * RB;          // one plane of the A stage
-  constexpr int BB = SG_BN * RB;          // one plane of the B stage
-  constexpr int STAGE = 2 * AB + 2 * BB;  // 40 / 80 KB
-  constexpr int RPI = 1024 / RB;          // rows per DMA instruction (16 / 8)
-  constexpr int LPR = RB / 16;            // lanes per row (4 / 8)
-  constexpr int AIW = SG_BM / RPI / 4;    // A instructions per plane per wave (2 / 4)
-  constexpr int BIW = SG_BN / RPI / 4;    // B instructions per plane per wave (3 / 6)
-  constexpr int DPW = 2 * (AIW + BIW);    // DMA instructions per wave per stage (10 / 20)
-  constexpr int SUB = KD / 32;            // 32-deep MFMA slices per stage
+  constexpr int RB = KD * 2;                  // LDS row bytes
+  constexpr int AB = SG_BM * RB;              // one plane of the A stage
+  constexpr int BB = SG_BN * RB;              // one plane of the B stage
+  constexpr int STAGE = NPL * (AB + BB);      // 40 KB (two planes, KD 32)
+  constexpr int RPI = 1024 / RB;              // rows per DMA instruction (16 / 8)
+  constexpr int LPR = RB / 16;                // lanes per row (4 / 8)
+  constexpr int AIW = SG_BM / RPI / 4;        // A instructions per plane per wave (2 / 4)
+  constexpr int BIW = SG_BN / RPI / 4;        // B instructions per plane per wave (3 / 6)
+  constexpr int DPW = NPL * (AIW + BIW);      // DMA instructions per wave per stage
+  constexpr int SUB = KD / 32;                // 32-deep MFMA slices per stage
   static_assert(NST * STAGE <= 163840 / OCC, "LDS");
+  static_assert((NST - 2) * DPW < 64, "vmcnt");
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -94,12 +103,12 @@ __global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P
 #pragma unroll
     for (int j = 0; j < AIW; ++j) {
       sg_glds16(asrc[j] + k0, base + (wave + 4 * j) * 1024);
-      sg_glds16(asrc[j] + P.a_lo + k0, base + AB + (wave + 4 * j) * 1024);
+      if constexpr (NPL == 2) sg_glds16(asrc[j] + P.a_lo + k0, base + AB + (wave + 4 * j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < BIW; ++j) {
-      sg_glds16(bsrc[j] + k0, base + 2 * AB + (wave + 4 * j) * 1024);
-      sg_glds16(bsrc[j] + P.w_lo + k0, base + 2 * AB + BB + (wave + 4 * j) * 1024);
+      sg_glds16(bsrc[j] + k0, base + NPL * AB + (wave + 4 * j) * 1024);
+      if constexpr (NPL == 2) sg_glds16(bsrc[j] + P.w_lo + k0, base + 2 * AB + BB + (wave + 4 * j) * 1024);
     }
   };
 
@@ -132,21 +141,25 @@ __global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         ah[i] = *reinterpret_cast<const bf16x8*>(base + aoff + i * 16 * RB);
-        al[i] = *reinterpret_cast<const bf16x8*>(base + AB + aoff + i * 16 * RB);
+        if constexpr (NPL == 2) al[i] = *reinterpret_cast<const bf16x8*>(base + AB + aoff + i * 16 * RB);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + boff + j * 16 * RB);
-        bl[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + BB + boff + j * 16 * RB);
+        bh[j] = *reinterpret_cast<const bf16x8*>(base + NPL * AB + boff + j * 16 * RB);
+        if constexpr (NPL == 2) bl[j] = *reinterpret_cast<const bf16x8*>(base + 2 * AB + BB + boff + j * 16 * RB);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = mfma16<PREC_BF16>(al[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma16<PREC_BF16>(ah[i], bl[j], acc[i][j]);
-          acc[i][j] = mfma16<PREC_BF16>(ah[i], bh[j], acc[i][j]);
+          if constexpr (NPL == 2) {
+            acc[i][j] = mfma16<PREC_BF16>(al[i], bh[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_BF16>(ah[i], bl[j], acc[i][j]);
+            acc[i][j] = mfma16<PREC_BF16>(ah[i], bh[j], acc[i][j]);
+          } else {
+            acc[i][j] = mfma16<PREC>(ah[i], bh[j], acc[i][j]);
+          }
         }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -180,6 +193,14 @@ __global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P
         const float4 bv = *reinterpret_cast<const float4*>(P.bias + n0 + n);
         v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
       }
+      if constexpr (NPL == 1) {
+        if (P.oplane) {  // (no residual / scale with a plane output, as wconv2)
+          u16* d = P.oplane + (int64_t)gm * P.ldo + n0 + n;
+          op_store2<PREC>(d, 0, f32x2{v.x, v.y});
+          op_store2<PREC>(d + 2, 0, f32x2{v.z, v.w});
+          continue;
+        }
+      }
       if (P.res) {
         const float4 rv = *reinterpret_cast<const float4*>(P.res + (int64_t)gm * P.ldr + n0 + n);
         v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
@@ -189,6 +210,16 @@ __global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P
     }
     __syncthreads();
   }
+}
+
+template <int KD, int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void sgemm_planes_kernel(const SGemmDev P) {
+  sg_body<KD, NST, OCC, 2, PREC_BF16>(P);
+}
+
+template <int KD, int NST, int PREC>
+__global__ __launch_bounds__(256, 2) void lin_plane_kernel(const SGemmDev P) {
+  sg_body<KD, NST, 2, 1, PREC>(P);
 }
 
 // fp32 rows [rows][C] (optionally x * scale[b][c] + shift[b][c], b = row / T: a GroupNorm affine) -> bf16 hi plane
@@ -235,6 +266,50 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 }
 
 bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K && knobs().sgemm; }
+
+// 1x1 conv / linear on one operand plane (ALCM_LIN1: 1 = 32-deep stages in a 4-deep ring, 2 = 64-deep stages double-
+// buffered, 0 = off: wconv2).  Eligible: f16 / bf16, k = 1 without padding, Cp % 32 == 0, N % 192 == 0, no GEGLU /
+// strided / activated / accumulated output.  Returns 1 when it launched.
+int lin_plane_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
+  const int v = knobs().lin1;
+  if (v <= 0 || (a.prec != PREC_F16 && a.prec != PREC_BF16)) return 0;
+  if (a.ksize != 1 || a.pad != 0 || a.out_stride > 0 || a.geglu_plane || a.out_act || a.accumulate || a.Cp % 32 ||
+      a.N % SG_BN || a.kpad < a.Cp || a.kpad % 8)
+    return 0;
+  if (a.out_plane ? (a.out || a.res) : !a.out) return 0;
+  auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  if (!al16(a.a) || !al16(wplane) || !al16(a.bias) || !al16(a.res) || !al16(a.out) || (((uintptr_t)a.out_plane) & 7))
+    return 0;
+  const int64_t M = (int64_t)a.B * a.T;
+  const int64_t nwg = (M + SG_BM - 1) / SG_BM * (a.N / SG_BN);
+  if (M >= (1ll << 31) || nwg >= (1ll << 30) || M * a.N >= (1ll << 40)) return 0;
+  SGemmDev P{};
+  P.a = (const u16*)a.a; P.w = wplane;
+  P.M = (int)M; P.N = a.N; P.K = a.Cp; P.kpad = a.kpad;
+  P.bias = a.bias; P.res = a.res; P.ldr = a.N; P.out = a.out; P.ldo = a.N; P.out_scale = a.out_scale;
+  P.oplane = (u16*)a.out_plane;
+  P.tiles_n = a.N / SG_BN;
+  P.nwg = (int)nwg;
+  void* tok = prof_start(s);
+  const bool f16 = a.prec == PREC_F16;
+  const bool deep = v == 2 && a.Cp % 64 == 0;
+  if (deep) {
+    if (f16) hipLaunchKernelGGL((lin_plane_kernel<64, 2, PREC_F16>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((lin_plane_kernel<64, 2, PREC_BF16>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+  } else {
+    if (f16) hipLaunchKernelGGL((lin_plane_kernel<32, 4, PREC_F16>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((lin_plane_kernel<32, 4, PREC_BF16>), dim3((unsigned)nwg), dim3(256), 0, s, P);
+  }
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::lin_plane_kernel<%d, %d, %d>", deep ? 64 : 32, deep ? 2 : 4, a.prec);
+    if (knobs().prof_shapes)
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " M%d N%d K%d", P.M, a.N, a.Cp);
+    prof_stop(tok, s, name, flops, bytes);
+  }
+  ALCM_HIP(hipGetLastError());
+  return 1;
+}
 
 
 int sgemm_planes(const u16* a, int64_t a_lo, int M, int K, const u16* w, int64_t w_lo, int kpad, int N,

@@ -671,6 +671,7 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
                 : 256;
   }
   const bool fills = (int64_t)a.B * mt256 * (a.N / W3_BN) >= g_ncu;
+  if (!off && (a.out_plane || (int64_t)a.B * a.T >= 1024) && lin_plane_try(a, wplane, flops, bytes, s)) return 1;
   if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || (full && fills)) &&
       wconv3_try(a, wplane, flops, bytes, s))
     return 1;

@@ -346,7 +346,7 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
            act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False,
-           strided: Optional[tuple] = None, dense: bool = False):
+           strided: Optional[tuple] = None, dense: bool = False, out_plane: bool = False):
     """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
 
     act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
@@ -354,7 +354,9 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     strided = (out, stride, offset, pad): one ConvTranspose1d phase, row t -> row t*stride + offset of the
     fp32 (B, R, N) tensor `out` (written in place and returned), input rows t - pad + tap*dilation.
     dense = True: the narrow-stage resident-weight kernel (alcm_opconv_dense): weights packed with cpad = C_real
-    (pack_conv_weight(w)), planes channels >= C_real ignored, the fused Activation1d writes channels < N only."""
+    (pack_conv_weight(w)), planes channels >= C_real ignored, the fused Activation1d writes channels < N only.
+    out_plane = True: conv + bias as one PREC operand plane (1, B, T, N) instead of the fp32 output (no residual /
+    activation / accumulate; the DiT q,k,v projection)."""
     npl, B, T, Cp = planes.shape
     assert planes.dtype == torch.int16 and planes.is_contiguous()
     N, cin, k = w.shape
@@ -383,6 +385,11 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     a.out, a.out_act, a.accumulate, a.out_scale, a.prec = ptr(out), out_act, int(accumulate_into is not None), \
         out_scale, int(prec)
     keep = []
+    if out_plane:
+        op = torch.empty((1, B, T, N), dtype=torch.int16, device=planes.device)
+        a.out, a.out_plane = None, ptr(op)
+        check(lib().alcm_opconv(C.byref(a), stream_handle()), "opconv")
+        return op
     if geglu:  # GEGLU epilogue (interleaved value/gate output columns) -> operand plane (1, B, T, N/2)
         gp = torch.empty((1, B, T, N // 2), dtype=torch.int16, device=planes.device)
         a.out, a.geglu_plane = None, ptr(gp)

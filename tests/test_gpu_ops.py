@@ -472,6 +472,42 @@ def test_wconv2_geglu_plane(K, T, prec):
     assert rel_l2(got.numpy(), ref.numpy()) < TOL[prec] * 4
 
 
+@pytest.mark.parametrize("C,N,T,mode", [(576, 1728, 467, "plane"), (576, 576, 467, "res"), (768, 384, 1000, "plain"),
+                                         (256, 192, 700, "plane"), (1536, 768, 520, "res")])
+@pytest.mark.parametrize("prec", [0, 2])
+def test_lin_plane_k1(K, C, N, T, mode, prec, monkeypatch):
+    """1x1 convs on one operand plane (alcm_sgemm.hip lin_plane_kernel: the DiT q,k,v projection with its plane
+    output, to_out with residual + scale) vs F.conv1d, and vs the two-workgroup wide conv (ALCM_LIN1=0) bit for bit
+    (same 32-deep slice order), in both ring builds (ALCM_LIN1=1 / 2); B * T is not a multiple of the 128-row tile."""
+    from audiolcm_amd import _hip
+    B = 2
+    x = _r((B, T, C), 180)
+    w, bias = _r((N, C, 1), 181, 1.0 / np.sqrt(C)), _r((N,), 182, 0.05)
+    r = _r((B, T, N), 183)
+    pl = K.operand_planes(dev(x), prec)
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias).permute(0, 2, 1)
+
+    def run():
+        if mode == "plane":
+            y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, out_plane=True)
+            return (y.view(torch.float16) if prec == 2 else y.view(torch.bfloat16)).float().cpu()[0]
+        if mode == "res":
+            return K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r), out_scale=0.5).cpu()
+        return K.opconv(pl, C, dev(w), dev(bias), 1, prec).cpu()
+    outs = {}
+    for v in ("1", "2", "0"):
+        monkeypatch.setenv("ALCM_LIN1", v)
+        _hip.reload_knobs()
+        try:
+            outs[v] = run()
+        finally:
+            monkeypatch.delenv("ALCM_LIN1")
+            _hip.reload_knobs()
+    want = (ref + r) * 0.5 if mode == "res" else ref
+    assert rel_l2(outs["1"].numpy(), want.numpy()) < TOL[prec] * (4 if mode == "plane" else 1)
+    assert torch.equal(outs["1"], outs["0"]) and torch.equal(outs["2"], outs["0"])
+
+
 @pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
                                                  (192, 96, 900, 2, 2), (96, 48, 333, 2, 0)])
 def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
