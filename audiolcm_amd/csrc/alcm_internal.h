@@ -134,8 +134,8 @@ struct Knobs {
   int text_flash = 1;            // ALCM_TEXT_FLASH: text-encoder attention in the fused kernel (0 = GEMM + softmax + GEMM)
   int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)
   int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs
-  int lin1 = 1;                  // ALCM_LIN1: single-plane 1x1 convs on lin_plane_kernel (1: 32-deep 4-stage ring, 2: 64-deep
-                                 // double-buffered), 0 = wconv2
+  int lin1 = -1;                 // ALCM_LIN1: single-plane 1x1 convs on lin_plane_kernel (1: 32-deep 4-stage ring, 2: 64-deep
+                                 // double-buffered, -1: 64-deep for plane outputs), 0 = wconv2
   int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip), 0 = gemm_kernel
   int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
   bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)

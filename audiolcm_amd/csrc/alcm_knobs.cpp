@@ -46,7 +46,7 @@ static Knobs read_knobs() {
   k.tconv_stagger = env_int("ALCM_TCONV_STAGGER", -1);
   k.post_planes = env_set("ALCM_POST_PLANES");
   k.sgemm = env_int("ALCM_SGEMM", 1);
-  k.lin1 = env_int("ALCM_LIN1", 1);
+  k.lin1 = env_int("ALCM_LIN1", -1);
   k.ups2 = env_int("ALCM_UPS2", 1);
   k.act3 = env_int("ALCM_ACT3", 1);
   k.text_flash = env_int("ALCM_TEXT_FLASH", 1);

@@ -268,11 +268,18 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K && knobs().sgemm; }
 
 // 1x1 conv / linear on one operand plane (ALCM_LIN1: 1 = 32-deep stages in a 4-deep ring, 2 = 64-deep stages double-
-// buffered, 0 = off: wconv2).  Eligible: f16 / bf16, k = 1 without padding, Cp % 32 == 0, N % 192 == 0, no GEGLU /
-// strided / activated / accumulated output.  Returns 1 when it launched.
+// buffered, 0 = off: wconv2, -1 = by shape: the 64-deep build for plane outputs only).  Measured per step at B = 32
+// (gpurun_out/r4ag): DiT q,k,v (N = 1728, plane output) 1.04 ms on wconv2 -> 0.84 (ring) / 0.75 (64-deep); DiT
+// to_out (N = 576, fp32 output + residual, one round of 351 tiles, bound by its epilogue) 0.55 -> 0.62 / 0.60.
+// Eligible: f16 / bf16, k = 1 without padding, Cp % 32 == 0, N % 192 == 0, no GEGLU / strided / activated /
+// accumulated output.  Returns 1 when it launched.
 int lin_plane_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
-  const int v = knobs().lin1;
-  if (v <= 0 || (a.prec != PREC_F16 && a.prec != PREC_BF16)) return 0;
+  int v = knobs().lin1;
+  if (v < 0) {
+    if (!a.out_plane) return 0;
+    v = 2;
+  }
+  if (v == 0 || (a.prec != PREC_F16 && a.prec != PREC_BF16)) return 0;
   if (a.ksize != 1 || a.pad != 0 || a.out_stride > 0 || a.geglu_plane || a.out_act || a.accumulate || a.Cp % 32 ||
       a.N % SG_BN || a.kpad < a.Cp || a.kpad % 8)
     return 0;

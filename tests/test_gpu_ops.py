@@ -495,7 +495,7 @@ def test_lin_plane_k1(K, C, N, T, mode, prec, monkeypatch):
             return K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r), out_scale=0.5).cpu()
         return K.opconv(pl, C, dev(w), dev(bias), 1, prec).cpu()
     outs = {}
-    for v in ("1", "2", "0"):
+    for v in ("1", "2", "0", "-1"):
         monkeypatch.setenv("ALCM_LIN1", v)
         _hip.reload_knobs()
         try:
@@ -505,7 +505,7 @@ def test_lin_plane_k1(K, C, N, T, mode, prec, monkeypatch):
             _hip.reload_knobs()
     want = (ref + r) * 0.5 if mode == "res" else ref
     assert rel_l2(outs["1"].numpy(), want.numpy()) < TOL[prec] * (4 if mode == "plane" else 1)
-    assert torch.equal(outs["1"], outs["0"]) and torch.equal(outs["2"], outs["0"])
+    assert all(torch.equal(outs[v], outs["0"]) for v in ("1", "2", "-1"))
 
 
 @pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
