@@ -233,7 +233,7 @@ struct AmGeo {
   static_assert(XR <= AM_XS && (SS / 4) % 2 == 1 && 8 * (UPB - 1) + 15 < XR && TT % 16 == 0, "act_mfma tile");
 };
 
-template <int TT>
+template <int TT, bool DEFER>
 __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const float* __restrict__ x,
                                                                           u16* __restrict__ y, int T, int C, int Cp,
                                                                           const float* __restrict__ aexp,
@@ -307,6 +307,18 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   };
   load_x(tile0 * AM_TT);
   u16* const yb = y + (int64_t)b * T * Cp + ct * 64;
+  // the output tile staged in ob goes out one iteration late, issued BEFORE the next prefetch: the compiler waits for a
+  // tile's x rows with vmcnt(0) at the loop head, and stores issued after the prefetch (at the end of the tile) made
+  // that wait drain their round trip every tile; issued before it, they are a whole tile old by then
+  auto store_tile = [&](int t0) {
+#pragma unroll
+    for (int k = 0; k < AM_TT * 8 / 256; ++k) {
+      const int e = tid + 256 * k, r = e >> 3, sg = e & 7;
+      if (t0 + r < T)
+        *reinterpret_cast<uint4*>(yb + (int64_t)(t0 + r) * Cp + sg * 8) =
+            *reinterpret_cast<const uint4*>(ob + r * OS + sg * 8);
+    }
+  };
   for (int tl = 0; tl < ntile; ++tl) {
     const int t0 = (tile0 + tl) * AM_TT;
     // (v, v) fp16 pairs at xw'[c * XS + r] of the owning wave w'
@@ -322,6 +334,7 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
         xo[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
       }
     }
+    if (DEFER && tl > 0) store_tile(t0 - AM_TT);  // (ob is rewritten only after the barrier below)
     if (tl + 1 < ntile) load_x(t0 + AM_TT);
     // every wave's x pairs staged: LDS-only wait (a __syncthreads fence would also wait for the prefetch)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -374,21 +387,15 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
       w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
       *reinterpret_cast<uint2*>(ob + (16 * d + l16) * OS + wave * 16 + 4 * q4) = w;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's 16 channels of the tile staged
-#pragma unroll
-    for (int k = 0; k < AM_TT * 8 / 256; ++k) {
-      const int e = tid + 256 * k, r = e >> 3, sg = e & 7;
-      if (t0 + r < T)
-        *reinterpret_cast<uint4*>(yb + (int64_t)(t0 + r) * Cp + sg * 8) =
-            *reinterpret_cast<const uint4*>(ob + r * OS + sg * 8);
-    }
-    // the staged tile and the x pairs read out before the next tile overwrites them (LDS only: the stores and the
-    // prefetch stay in flight)
+    // every wave's 16 channels of the tile staged, and every wave past its up reads of xs (the next tile's x pairs
+    // may be written)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // the next tile's x pairs overwrite xw only after this tile's up reads retired (same wave, in order)
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (!DEFER) {  // (ALCM_ACT_DEFER=0: the stores at the end of their own tile)
+      store_tile(t0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
   }
+  if (DEFER && ntile > 0) store_tile((tile0 + ntile - 1) * AM_TT);
 }
 
 bool act_mfma_ok(int C, int Cp, int prec) {
@@ -403,8 +410,9 @@ int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* 
   const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
   const int64_t nwg = (int64_t)B * strips_t * tiles_c;
   if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma: too large");
-  hipLaunchKernelGGL(act_mfma_kernel<TT>, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp,
-                     inv_beta, f, strips_t, tiles_c);
+  auto kern = knobs().act_defer ? act_mfma_kernel<TT, true> : act_mfma_kernel<TT, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp, inv_beta, f,
+                     strips_t, tiles_c);
   ALCM_HIP(hipGetLastError());
   return 0;
 }

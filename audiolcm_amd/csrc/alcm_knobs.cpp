@@ -57,6 +57,7 @@ static Knobs read_knobs() {
   k.ampair_ablate = env_int("ALCM_AMPAIR_ABLATE", 0);
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
+  k.act_defer = env_int("ALCM_ACT_DEFER", 1);
   return k;
 }
 

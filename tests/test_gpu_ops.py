@@ -721,3 +721,12 @@ def test_activation1d_mfma(K, C, T, monkeypatch):
     print(f"act C{C} T{T}: mfma {e_mfma:.2e} valu {e_valu:.2e} mfma-vs-valu {rel_l2(got.numpy(), valu.numpy()):.2e}")
     assert torch.isfinite(got).all()
     assert e_mfma < 1e-3 and e_mfma < 2.5 * e_valu
+    # the stores at the end of their own tile (ALCM_ACT_DEFER=0) instead of one tile late: the same values
+    monkeypatch.setenv("ALCM_ACT_DEFER", "0")
+    _hip.reload_knobs()
+    try:
+        inl = K.activation1d_op(xd, dev(a), dev(bt), f, f, 2).cpu()[0].view(torch.float16).float()
+    finally:
+        monkeypatch.delenv("ALCM_ACT_DEFER")
+        _hip.reload_knobs()
+    assert torch.equal(got, inl)
