@@ -224,6 +224,17 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   float* ot = reinterpret_cast<float*>(smem);
   constexpr int cq = BN / 4;
   constexpr int PER = 64 * cq / 256;  // float4 per thread per slice (12 / 6)
+  // GEGLU: this thread's bias columns (the same in every slice), loaded once up front: loaded next to each store they
+  // made every store-load pair a vmcnt(0) round trip (24 serialised per tile)
+  float4 gbv[GEGLU ? PER : 1];
+  if constexpr (GEGLU) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int idx = tid + e * 256;
+      const int n = (idx - (idx / cq) * cq) * 4;
+      gbv[e] = P.bias ? *reinterpret_cast<const float4*>(P.bias + col0 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   for (int h = 0; h < WGM; ++h) {
     if (wm == h) {
 #pragma unroll
@@ -243,21 +254,18 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int m = idx / cq, n = (idx - m * cq) * 4;
         if (r0 + m >= P.T) continue;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        if (P.bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
-          v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-        }
+        v.x += gbv[e].x; v.y += gbv[e].y; v.z += gbv[e].z; v.w += gbv[e].w;
         f32x2 y;
         y.x = v.x * alcm_act(v.y, ACT_GELU_ERF);
         y.y = v.z * alcm_act(v.w, ACT_GELU_ERF);
         op_store2<PREC>(P.gplane + ((int64_t)b * P.T + r0 + m) * No + (col0 + n) / 2, 0, y);
       }
     } else {
-      // two passes of PER/2 loads: the other half's accumulators are still live in half 0
-      constexpr int PH = PER / 2;
+      // passes of PH loads (residual, accumulate, bias): the other halves' accumulators are still live in half 0
+      constexpr int PH = BN == 192 ? PER / 4 : PER / 2;
 #pragma unroll
       for (int e0 = 0; e0 < PER; e0 += PH) {
-      float4 rv[PH], pv[PH];
+      float4 rv[PH], pv[PH], bv[PH];  // (bias with them: loaded next to each store it cost a vmcnt(0) per store)
 #pragma unroll
       for (int e = 0; e < PH; ++e) {
         const int idx = tid + (e0 + e) * 256;
@@ -266,6 +274,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + min(col0 + n, P.N - 4);
         rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
         pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[e] = P.bias ? *reinterpret_cast<const float4*>(P.bias + min(col0 + n, P.N - 4))
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int e = 0; e < PH; ++e) {
@@ -274,10 +284,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         if (r0 + m >= P.T || col0 + n >= P.N) continue;
         const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        if (P.bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(P.bias + col0 + n);
-          v.x += bv.x; v.y += bv.y; v.z += bv.z; v.w += bv.w;
-        }
+        v.x += bv[e].x; v.y += bv[e].y; v.z += bv[e].z; v.w += bv[e].w;
         if (P.oplane) {  // plane output (no residual / accumulate / act): 4 rounded values, one 8-B store
           op_store2<PREC>(P.oplane + go, 0, f32x2{v.x, v.y});
           op_store2<PREC>(P.oplane + go + 2, 0, f32x2{v.z, v.w});
