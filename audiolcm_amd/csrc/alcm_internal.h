@@ -149,7 +149,6 @@ struct Knobs {
   int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
   int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
   int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
-  int wconv2_epi = 0;            // ALCM_WCONV2_EPI: 1 = wconv2 loads the bias next to each store (the old epilogue, A/B)
   int act_defer = 1;             // ALCM_ACT_DEFER: act_mfma issues a tile's plane stores one tile late, before the next
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)

@@ -58,7 +58,6 @@ static Knobs read_knobs() {
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
-  k.wconv2_epi = env_int("ALCM_WCONV2_EPI", 0);
   return k;
 }
 

@@ -39,7 +39,6 @@ struct WConvDev {
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int out_act;          // wconv2: activation of acc + bias (ALCM_ACT_*, 0 = none)
   u16* oplane;          // wconv2: conv + bias as an operand plane [B][T][N] (PREC) instead of the fp32 output
-  int epi_inline;       // wconv2 (ALCM_WCONV2_EPI=1, A/B): bias loaded next to each store, as before round 4's fix
 };
 
 
@@ -231,7 +230,6 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   if constexpr (GEGLU) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      if (P.epi_inline) break;
       const int idx = tid + e * 256;
       const int n = (idx - (idx / cq) * cq) * 4;
       gbv[e] = P.bias ? *reinterpret_cast<const float4*>(P.bias + col0 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -256,9 +254,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int m = idx / cq, n = (idx - m * cq) * 4;
         if (r0 + m >= P.T) continue;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        const float4 b4 = !P.epi_inline ? gbv[e]
-                          : P.bias ? *reinterpret_cast<const float4*>(P.bias + col0 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-        v.x += b4.x; v.y += b4.y; v.z += b4.z; v.w += b4.w;
+        v.x += gbv[e].x; v.y += gbv[e].y; v.z += gbv[e].z; v.w += gbv[e].w;
         f32x2 y;
         y.x = v.x * alcm_act(v.y, ACT_GELU_ERF);
         y.y = v.z * alcm_act(v.w, ACT_GELU_ERF);
@@ -278,8 +274,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int64_t go = ((int64_t)b * P.orows + (int64_t)t * P.ostride + P.ooff) * P.N + min(col0 + n, P.N - 4);
         rv[e] = P.res ? *reinterpret_cast<const float4*>(P.res + go) : make_float4(0.f, 0.f, 0.f, 0.f);
         pv[e] = P.accumulate ? *reinterpret_cast<const float4*>(P.out + go) : make_float4(0.f, 0.f, 0.f, 0.f);
-        bv[e] = P.bias && !P.epi_inline ? *reinterpret_cast<const float4*>(P.bias + min(col0 + n, P.N - 4))
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[e] = P.bias ? *reinterpret_cast<const float4*>(P.bias + min(col0 + n, P.N - 4))
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int e = 0; e < PH; ++e) {
@@ -288,8 +284,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         if (r0 + m >= P.T || col0 + n >= P.N) continue;
         const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
-        const float4 b4 = P.epi_inline && P.bias ? *reinterpret_cast<const float4*>(P.bias + col0 + n) : bv[e];
-        v.x += b4.x; v.y += b4.y; v.z += b4.z; v.w += b4.w;
+        v.x += bv[e].x; v.y += bv[e].y; v.z += bv[e].z; v.w += bv[e].w;
         if (P.oplane) {  // plane output (no residual / accumulate / act): 4 rounded values, one 8-B store
           op_store2<PREC>(P.oplane + go, 0, f32x2{v.x, v.y});
           op_store2<PREC>(P.oplane + go + 2, 0, f32x2{v.z, v.w});
@@ -712,7 +707,6 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     P.gplane = (u16*)a.geglu_plane;
     P.out_act = a.out_act;
     P.oplane = (u16*)a.out_plane;
-    P.epi_inline = knobs().wconv2_epi;
     P.ostride = strided ? a.out_stride : 1;
     P.ooff = strided ? a.out_offset : 0;
     P.orows = strided ? a.out_rows : a.T;
