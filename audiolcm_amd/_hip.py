@@ -88,6 +88,7 @@ _SIGS = [
     ("alcm_softmax_rows", C.c_int, [fp, C.c_int, C.c_int, i64, vp]),
     ("alcm_activation1d", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, i64, i64, fp, fp, fp, fp, vp]),
     ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
+    ("alcm_activation1d_op_f16in", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_opconv_dense", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_ampblock_pair", C.c_int, [C.POINTER(AmpairArgs), vp]),

@@ -233,8 +233,10 @@ struct AmGeo {
   static_assert(XR <= AM_XS && (SS / 4) % 2 == 1 && 8 * (UPB - 1) + 15 < XR && TT % 16 == 0, "act_mfma tile");
 };
 
-template <int TT, bool DEFER>
-__global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const float* __restrict__ x,
+// IN16: x is an fp16 plane [B][T][C] (a conv1 that wrote its output in the format this kernel rounds its input to:
+// the same (v, v) pairs, half the bytes read)
+template <int TT, bool DEFER, bool IN16 = false>
+__global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const void* __restrict__ xin,
                                                                           u16* __restrict__ y, int T, int C, int Cp,
                                                                           const float* __restrict__ aexp,
                                                                           const float* __restrict__ ibeta,
@@ -295,14 +297,17 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
   // w's instruction it covers rows 16 it + 4 w .. + 3, lane = (row, 16-B piece); each piece belongs to the wave
   // owning its 16 channels.  The next tile's rows are loaded into registers while this tile computes
   // (each wave loading its own 16 channels as 64-B row pieces measured 8.32 vs 8.18 ms/step, profiles/r4ae)
-  const float* xb = x + (int64_t)b * T * C + ct * 64 + (lane & 15) * 4;
-  float4 xv[AM_XR / 16];
+  // (IN16: the same lanes and rows, 8-B pieces of four fp16 channels: 128-B row segments)
+  typedef typename std::conditional<IN16, uint2, float4>::type XPiece;
+  const char* const xb = reinterpret_cast<const char*>(xin) +
+                         ((int64_t)b * T * C + ct * 64 + (lane & 15) * 4) * (IN16 ? 2 : 4);
+  XPiece xv[AM_XR / 16];
   auto xrow = [&](int it) { return it * 16 + wave * 4 + (lane >> 4); };
   auto load_x = [&](int t0) {
 #pragma unroll
     for (int it = 0; it < AM_XR / 16; ++it) {
       const int t = min(max(t0 - 5 + xrow(it), 0), T - 1);
-      xv[it] = *reinterpret_cast<const float4*>(xb + (int64_t)t * C);
+      xv[it] = *reinterpret_cast<const XPiece*>(xb + (int64_t)t * C * (IN16 ? 2 : 4));
     }
   };
   load_x(tile0 * AM_TT);
@@ -328,10 +333,18 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const f
 #pragma unroll
       for (int it = 0; it < AM_XR / 16; ++it) {
         const int r = xrow(it);
-        xo[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
-        xo[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
-        xo[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
-        xo[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+        if constexpr (IN16) {
+          const uint2 h = xv[it];
+          xo[(c + 0) * AM_XS + r] = (h.x & 0xffffu) | (h.x << 16);
+          xo[(c + 1) * AM_XS + r] = (h.x >> 16) | (h.x & 0xffff0000u);
+          xo[(c + 2) * AM_XS + r] = (h.y & 0xffffu) | (h.y << 16);
+          xo[(c + 3) * AM_XS + r] = (h.y >> 16) | (h.y & 0xffff0000u);
+        } else {
+          xo[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
+          xo[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
+          xo[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
+          xo[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+        }
       }
     }
     if (DEFER && tl > 0) store_tile(t0 - AM_TT);  // (ob is rewritten only after the barrier below)
@@ -402,15 +415,16 @@ bool act_mfma_ok(int C, int Cp, int prec) {
   return knobs().act_mfma && prec == PREC_F16 && C >= 192 && C % 64 == 0 && Cp == C;
 }
 
-int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
-             const Taps12O& f, hipStream_t s) {
+int act_mfma(const void* x, bool x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+             const float* inv_beta, const Taps12O& f, hipStream_t s) {
   if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 15)) return set_error(ALCM_E_INVALID, "act_mfma: alignment");
   constexpr int TT = 64;
   const int tiles_t = (T + TT - 1) / TT, tiles_c = C / 64;
   const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
   const int64_t nwg = (int64_t)B * strips_t * tiles_c;
   if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma: too large");
-  auto kern = knobs().act_defer ? act_mfma_kernel<TT, true> : act_mfma_kernel<TT, false>;
+  auto kern = x16 ? (knobs().act_defer ? act_mfma_kernel<TT, true, true> : act_mfma_kernel<TT, false, true>)
+                  : (knobs().act_defer ? act_mfma_kernel<TT, true> : act_mfma_kernel<TT, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, s, x, (u16*)y, T, C, Cp, alpha_exp, inv_beta, f,
                      strips_t, tiles_c);
   ALCM_HIP(hipGetLastError());

@@ -59,8 +59,13 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
                     hipStream_t s);
 // Activation1d with both FIRs on MFMA, fp16 planes out (alcm_act.hip; C >= 192, C % 64 == 0, PREC_F16, Cp == C)
 bool act_mfma_ok(int C, int Cp, int prec);
-int act_mfma(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp, const float* inv_beta,
-             const Taps12O& f, hipStream_t s);
+// x16: x is an fp16 plane [B][T][C] (the wide-stage conv1 output, alcm_opconv's out_plane) instead of fp32
+int act_mfma(const void* x, bool x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+             const float* inv_beta, const Taps12O& f, hipStream_t s);
+// Activation1d of an fp16 plane x16 [B][T][C] into fp16 planes (act_mfma shapes only; ALCM_E_INVALID otherwise)
+int activation1d_op_h16(const void* x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                        const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                        hipStream_t s);
 int nconv_try(const alcm_opconv_args& a, const unsigned short* wplane, const void* actepi, double flops, double bytes,
               hipStream_t s);
 int opconv(const alcm_opconv_args& a, hipStream_t s);
@@ -144,7 +149,7 @@ struct Knobs {
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
                                  // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv
   int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
-  int ampair = 1;                // ALCM_AMPAIR: BigVGAN stages 3-5 as fused AMPBlock half-layer pairs (alcm_ampair.hip),
+  int ampair = 0;                // ALCM_AMPAIR (opt-in): BigVGAN stages 3-5 as fused AMPBlock half-layer pairs (alcm_ampair.hip),
                                  // 0 = one launch per Activation1d / conv (tconv)
   int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
   int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
@@ -152,6 +157,9 @@ struct Knobs {
   int act_defer = 1;             // ALCM_ACT_DEFER: act_mfma issues a tile's plane stores one tile late, before the next
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
+  int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
+  int w3_var = 0;                // ALCM_W3_VAR: wconv3 SIMD-partner schedule (0 per-slice setprio, 1 static prio for
+                                 // waves 4-7, 2 static prio + waves 4-7 staggered by half a step)
 };
 const Knobs& knobs();
 

@@ -58,6 +58,8 @@ static Knobs read_knobs() {
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
+  k.w3_var = env_int("ALCM_W3_VAR", 0);
+  k.conv1_h16 = env_int("ALCM_CONV1_H16", 1);
   return k;
 }
 

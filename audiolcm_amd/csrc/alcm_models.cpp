@@ -1383,7 +1383,8 @@ static int amp_pair(hipStream_t s, const AmpW& A, size_t l, const float* x, floa
 
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
                       float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
-                      const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false) {
+                      const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false,
+                      void* out_plane = nullptr) {
   alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
   if (dense) {
@@ -1425,6 +1426,7 @@ static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int
   g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
   g.bias = cw.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate;
   g.out_scale = out_scale; g.prec = prec;
+  g.out_plane = out_plane;
   return opconv(g, s);
 }
 
@@ -1503,6 +1505,8 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const bool pair = dense && stage_ampair(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
+    // the wide stages' conv1 -> Activation1d hand-off as an fp16 plane (ALCM_CONV1_H16=0: fp32, the A/B reference)
+    const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
     // the three chains' first Activation1d in one pass over u (their own planes, same taps; ALCM_ACT3=0: one per chain)
     bool act3 = conc && fuse && !pair && S.rb.size() == 3 && knobs().act3 &&
                 !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
@@ -1552,8 +1556,18 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
           }
         } else {
           ALCM_TRY(act_planes(sj, A.act[2 * l], cur, w, B, To, S.cout, pamp, cb.pl));
-          ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, cb.t, 1.f, 0, 0, pamp, cb.pl));
-          ALCM_TRY(act_planes(sj, A.act[2 * l + 1], cb.t, w, B, To, S.cout, pamp, cb.pl));
+          if (h16) {
+            // conv1's only consumer is the next Activation1d, whose MFMA kernel rounds its input to fp16: conv1 writes
+            // that fp16 plane (into the fp32 scratch cb.t) and the activation reads it, bit-identical at half the bytes
+            ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl, nullptr,
+                                nullptr, false, cb.t));
+            const ActW& a2 = A.act[2 * l + 1];
+            ALCM_TRY(activation1d_op_h16(cb.t, cb.pl, B, To, S.cout, round_up(S.cout, 32), a2.aexp, a2.ibeta, a2.fup,
+                                         a2.fdn, pamp, sj));
+          } else {
+            ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, cb.t, 1.f, 0, 0, pamp, cb.pl));
+            ALCM_TRY(act_planes(sj, A.act[2 * l + 1], cb.t, w, B, To, S.cout, pamp, cb.pl));
+          }
           ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, last ? x : cb.rb, last ? inv : 1.f, last && j > 0, 0,
                               pamp, cb.pl));
           cur = cb.rb;

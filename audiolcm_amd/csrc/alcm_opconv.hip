@@ -119,6 +119,32 @@ int activation1d_x3(const float* x, void* const y[3], int B, int T, int C, int C
   return 0;
 }
 
+// Activation1d of an fp16 plane (the wide-stage AMPBlock conv1 written by alcm_opconv's out_plane epilogue): only
+// the MFMA kernel's shapes, whose FIR input is that fp16 value anyway (bit-identical to the fp32-input call on the
+// conv's fp32 output)
+int activation1d_op_h16(const void* x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                        const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                        hipStream_t s) {
+  if (!x16 || !y || !alpha_exp || !inv_beta || !up_filter || !down_filter || B <= 0 || T <= 0 || C <= 0)
+    return set_error(ALCM_E_INVALID, "activation1d_op_f16in: bad arguments");
+  if (!act_mfma_ok(C, Cp, prec) || (((uintptr_t)x16) & 15) || (((uintptr_t)y) & 15))
+    return set_error(ALCM_E_INVALID, "activation1d_op_f16in: needs prec F16, C >= 192, C % 64 == 0, Cp == C and "
+                                     "16-byte aligned x / y");
+  Taps12O f;
+  for (int k = 0; k < 12; ++k) {
+    f.up[k] = 2.0f * up_filter[k];
+    f.dn[k] = down_filter[k];
+  }
+  void* tok = prof_start(s);
+  ALCM_TRY(act_mfma(x16, true, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
+  if (tok) {
+    const double e = (double)B * T;
+    prof_stop(tok, s, knobs().act_defer ? "alcm::act_mfma_kernel<64, true, true>" : "alcm::act_mfma_kernel<64, false, true>",
+                2.0 * 36.0 * e * C, e * (2.0 * C + 2.0 * Cp));
+  }
+  return 0;
+}
+
 int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                     hipStream_t s) {
@@ -142,10 +168,11 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
   if (act_mfma_ok(C, Cp, prec) && !(((uintptr_t)x) & 15) && !(((uintptr_t)y) & 15)) {  // both FIRs on MFMA (alcm_act.hip): the wide stages under the mixed policy
     void* tok = prof_start(s);
-    ALCM_TRY(act_mfma(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
+    ALCM_TRY(act_mfma(x, false, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
     if (tok) {
       const double e = (double)B * T;
-      prof_stop(tok, s, "alcm::act_mfma_kernel<64>", 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp));
+      prof_stop(tok, s, knobs().act_defer ? "alcm::act_mfma_kernel<64, true, false>" : "alcm::act_mfma_kernel<64, false, false>",
+                2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp));
     }
     return 0;
   }
@@ -807,6 +834,13 @@ extern "C" int alcm_activation1d_op(const float* x, void* y, int B, int T, int C
                                     alcm_stream_t stream) {
   return alcm::activation1d_op(x, y, B, T, C, Cp, alpha_exp, inv_beta, up_filter, down_filter, prec,
                                (hipStream_t)stream);
+}
+
+extern "C" int alcm_activation1d_op_f16in(const void* x16, void* y, int B, int T, int C, int Cp,
+                                          const float* alpha_exp, const float* inv_beta, const float* up_filter,
+                                          const float* down_filter, int prec, alcm_stream_t stream) {
+  return alcm::activation1d_op_h16(x16, y, B, T, C, Cp, alpha_exp, inv_beta, up_filter, down_filter, prec,
+                                   (hipStream_t)stream);
 }
 
 extern "C" int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream) {

@@ -340,12 +340,23 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-template <int PREC>
+// VAR (ALCM_W3_VAR, MI355X_MICROARCH.md "Two waves per SIMD"): the two waves sharing a SIMD (w and w + 4) run the same
+// program through one barrier per step, so they reach their MFMA bursts, fragment-read bursts and the barrier together.
+//   0: s_setprio 1 around each slice's MFMA block (round 3);
+//   1: no per-segment flips, one static s_setprio 1 for waves 4-7 (the arbitration losers);
+//   2: 1 + waves 4-7 staggered by half a step: they run [slice 0, slice 1] of a step between two barriers (the slot's
+//      first-slice fragments read after the barrier that publishes it) where waves 0-3 run [slice 1 of step g, slice 0
+//      of step g + 1], so one wave's exposed fragment reads meet its partner's MFMA burst.
+// Every variant issues the same MFMAs on the same fragments in the same order per accumulator: bit-identical results.
+template <int PREC, int VAR>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches below)
   const int wm = wave >> 1, wn = wave & 1;
+  const bool late = VAR == 2 && wave >= 4;
+  if (VAR >= 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   const int ntiles = P.nwg;
@@ -463,6 +474,65 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
                                             (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
   };
 
+  // tile epilogue, straight from the accumulators: fp32 out = (acc + bias + res) * scale (+ out), or (oplane) the
+  // operand plane of acc + bias in the format of PREC (the AMPBlock conv1 whose only consumer, the next Activation1d,
+  // rounds its input to that format: the same rounding of the same fp32 value, half the bytes on both sides)
+  auto epilogue = [&](int ti) {
+    int b, t0, col0;
+    tile_of(ti, b, t0, col0);
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
+    if (P.oplane) {
+      // column pairs through a lane-pair exchange (DPP quad_perm [1, 0, 3, 2]): per accumulator row pair (r0, r1) the
+      // even lane of a pair stores row r0, columns (c, c + 1), the odd lane row r1, columns (c - 1, c): 4-B stores
+      const bool odd = lane & 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp) {
+          const int r = 2 * rp + (odd ? 1 : 0);
+          const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          u16* const rowp = P.oplane + ((int64_t)b * P.T + min(t, P.T - 1)) * P.N + col0 + wn * 96 + (lane & 14);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            // (+ 0.f: the fp32 epilogue's value, acc + bias + a zero residual, signed zeros included)
+            const float v0 = acc[i][j][2 * rp] + bv[j] + 0.f, v1 = acc[i][j][2 * rp + 1] + bv[j] + 0.f;
+            const float send = odd ? v0 : v1;
+            const float recv = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, true));
+            const float lo = odd ? recv : v0, hi = odd ? v1 : recv;
+            if (t < P.T) op_store2<PREC>(rowp + j * 16, 0, f32x2{lo, hi});
+          }
+        }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float rv[4][TN], pv[4][TN];
+      int orow[4];  // output row (b T + t) of each accumulator row, -1 where nothing is stored
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        orow[r] = t < P.T ? b * P.T + t : -1;
+        const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
+          pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (orow[r] < 0) continue;
+        const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
+      }
+    }
+  };
+
   // prologue: window 0, weights 0, 1, 2 (window 1 is issued in pieces during chunk 0)
   stage_win(0);
   issue_wt(0);
@@ -481,9 +551,33 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
 
   int ti = 0, c = 0, tap = 0, sl = 0, q = 0;  // q: global chunk (window buffer q & 1)
+  // ---- mid-step: weight step g + 1 (and at a chunk's last step the next chunk's window) resident in every wave's
+  //      share; every wave done reading this slot and, at a chunk's last step, this chunk's window.  Loads issued after
+  //      weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay in flight
+  auto mid_step = [&]() {
+    switch (pieces_last) {
+      case 0: w3_wait_barrier<W3_BPW>(); break;
+      case 1: w3_wait_barrier<W3_BPW + 1>(); break;
+      case 2: w3_wait_barrier<W3_BPW + 2>(); break;
+      default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
+    }
+    pieces_last = 0;
+    if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
+      if (tap == 0) win_setup(q + 1);
+      for (int j = tap; j < W3_WPW; j += wspread) {
+        win_piece(j);
+        ++pieces_last;
+      }
+    }
+  };
   for (int g = 0; g < total; ++g) {
+    const bool chunk_end = tap == K - 1;
+    const bool tile_end = chunk_end && c + 1 == nC;
+    const int sl1 = sl == 2 ? 0 : sl + 1;
+    const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
+    const int ntap = chunk_end ? 0 : tap + 1;
     // ---- slice 0: MFMAs on (aA, bA); slice 1's fragments (this slot, this window) read under them
-    __builtin_amdgcn_s_setprio(1);
+    if (VAR == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -501,52 +595,46 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
     __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (VAR == 0) __builtin_amdgcn_s_setprio(0);
 
-    // ---- mid-step: weight step g + 1 (and at a chunk's last step the next chunk's window) resident in every
-    //      wave's share; every wave done reading this slot and, at a chunk's last step, this chunk's window.  Loads
-    //      issued after weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay
-    //      in flight
-    const bool chunk_end = tap == K - 1;
-    switch (pieces_last) {
-      case 0: w3_wait_barrier<W3_BPW>(); break;
-      case 1: w3_wait_barrier<W3_BPW + 1>(); break;
-      case 2: w3_wait_barrier<W3_BPW + 2>(); break;
-      default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
-    }
-    pieces_last = 0;
-    if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
-      if (tap == 0) win_setup(q + 1);
-      for (int j = tap; j < W3_WPW; j += wspread) {
-        win_piece(j);
-        ++pieces_last;
+    if (!late) {
+      mid_step();
+      // ---- slice 1: MFMAs on (aB, bB); the next step's slice-0 fragments read under them
+      // (after the last step these re-read resident LDS: harmless)
+      if (VAR == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+        if (i == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+#pragma unroll
+          for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+          // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
+          issue_wt(sl);
+        }
       }
+      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+      __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
+      if (VAR == 0) __builtin_amdgcn_s_setprio(0);
+    } else {
+      // ---- waves 4-7 (VAR 2): slice 1 right behind slice 0 (its fragments are in registers), then the mid-step
+      //      barrier; the next step's slice-0 fragments are read after it (the slot it publishes)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      mid_step();
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+      issue_wt(sl);
     }
-
-    // ---- slice 1: MFMAs on (aB, bB); the next step's slice-0 fragments read under them
-    const int sl1 = sl == 2 ? 0 : sl + 1;
-    const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
-    const int ntap = chunk_end ? 0 : tap + 1;
-    // (after the last step these re-read resident LDS: harmless)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
-      if (i == 0) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
-#pragma unroll
-        for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
-        // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
-        issue_wt(sl);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
-    __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
-    __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-    __builtin_amdgcn_s_setprio(0);
     advance_wt();
 
     sl = sl1;
@@ -557,38 +645,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     tap = 0;
     ++q;
     if (++c == nC) {
-      // ---- tile epilogue, straight from the accumulators (fp32 out = (acc + bias + res) * scale (+ out))
-      {
-        int b, t0, col0;
-        tile_of(ti, b, t0, col0);
-        float bv[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          float rv[4][TN], pv[4][TN];
-          int orow[4];  // output row (b T + t) of each accumulator row, -1 where nothing is stored
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-            orow[r] = t < P.T ? b * P.T + t : -1;
-            const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
-              pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (orow[r] < 0) continue;
-            const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
-          }
-        }
-      }
+      epilogue(ti);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -605,9 +662,10 @@ static int g_ncu = 0;
 // residual, scale, accumulate; no GEGLU / strided output).  Returns 1 when it launched.
 static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
-  if (a.out_act || a.out_stride > 0 || a.geglu_plane || !a.out || a.Cp % 64 || a.ksize < 3 ||
-      (a.ksize - 1) * a.dil > 64 || a.N % W3_BN)
+  if (a.out_act || a.out_stride > 0 || a.geglu_plane || a.Cp % 64 || a.ksize < 3 || (a.ksize - 1) * a.dil > 64 ||
+      a.N % W3_BN)
     return 0;
+  if (a.out_plane ? (a.out || a.res || a.accumulate || (((uintptr_t)a.out_plane) & 3)) : !a.out) return 0;
   if (!g_ncu) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
@@ -621,6 +679,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   P.T = a.T; P.Cp = a.Cp; P.ksize = a.ksize; P.dil = a.dil; P.pad = a.pad;
   P.w = wplane; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
+  P.oplane = (u16*)a.out_plane;
   P.tiles_per_batch = (P.T + W3_BM - 1) / W3_BM;
   P.tiles_n = a.N / W3_BN;
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
@@ -633,11 +692,18 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
-  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
+  const int var = knobs().w3_var;
+  auto go = [&](auto vc) {
+    constexpr int V = decltype(vc)::value;
+    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, V>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, V>), dim3(grid), dim3(512), 0, s, P);
+  };
+  if (var == 1) go(std::integral_constant<int, 1>{});
+  else if (var == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 0>{});
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, %d>", a.prec, var == 1 || var == 2 ? var : 0);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);

@@ -342,6 +342,22 @@ def activation1d_op(x_cl: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
     return y
 
 
+def activation1d_op_f16in(x16: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor, up_filter: torch.Tensor,
+                          down_filter: torch.Tensor, prec: int) -> torch.Tensor:
+    """Activation1d of an fp16 operand plane (1, B, T, C) int16 (an `opconv(..., out_plane=True)` result) into
+    operand planes (1, B, T, C): alcm_activation1d_op_f16in (the wide-stage conv1 -> Activation1d hand-off)."""
+    _, B, T, Cc = x16.shape
+    assert x16.dtype == torch.int16 and x16.is_contiguous()
+    ae, ib = snake_params(alpha, beta)
+    ae, ib = ae.contiguous(), ib.contiguous()
+    fu = up_filter.detach().reshape(-1).float().cpu().contiguous()
+    fd = down_filter.detach().reshape(-1).float().cpu().contiguous()
+    y = torch.empty((1, B, T, Cc), dtype=torch.int16, device=x16.device)
+    check(lib().alcm_activation1d_op_f16in(ptr(x16), ptr(y), B, T, Cc, Cc, ptr(ae), ptr(ib), fu.data_ptr(),
+                                           fd.data_ptr(), int(prec), stream_handle()), "activation1d_op_f16in")
+    return y
+
+
 def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,

@@ -157,6 +157,15 @@ int alcm_activation1d(const float* x, float* y, int B, int T, int C, int64_t sb,
 int alcm_activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                          const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
                          alcm_stream_t stream);
+/* alcm_activation1d_op_f16in: alcm_activation1d_op (alias_free_torch/act.py:23-27) of an fp16 plane x16 [B][T][C]
+ *   DEVICE — the BigVGAN AMPBlock conv1 output written by alcm_opconv's out_plane epilogue (vocoder/bigvgan/
+ *   models.py:74-79: that conv's only consumer is this activation) — into fp16 planes y [B][T][C].  Only the shapes
+ *   whose FIR input alcm_activation1d_op rounds to fp16 anyway: prec ALCM_PREC_F16, C >= 192, C % 64 == 0, Cp == C,
+ *   16-byte aligned x16 / y; the result equals alcm_activation1d_op on the fp32 conv output bit for bit.
+ *   ALCM_E_INVALID otherwise. */
+int alcm_activation1d_op_f16in(const void* x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
+                               const float* inv_beta, const float* up_filter, const float* down_filter, int prec,
+                               alcm_stream_t stream);
 /* alcm_opconv: out (B,T,N) = conv_{ksize,dil}(a) with same-length zero padding (2*pad == (ksize-1)*dil)
  * on operand planes a (as written by alcm_activation1d_op, lo plane a_lo_off elements after hi), weights
  * packed by alcm_pack_conv_weight with cpad = Cp; epilogue as alcm_gemm: v = acc + bias[n];

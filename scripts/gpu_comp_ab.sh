@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of knob settings on bench.py's SURVEY §8(f) component lines (text encoders, mel + Encoder1D), alternating,
-# two rounds.  Usage: bash scripts/gpu_comp_ab.sh <tag> "<variant> ..." (variant as in gpu_r4.sh)
+# two rounds.  Usage: bash scripts/gpu_comp_ab.sh <tag> "<variant> ..." (variant as in gpu_run.sh)
 tag=${1:-comp}
 variants=${2:-"-"}
 out=gpurun_out/$tag; mkdir -p $out

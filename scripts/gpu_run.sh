@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 GPU call: selected GPU tests, optional microbench modes, then an A/B of knob settings on the default bench
+# GPU call: selected GPU tests, optional microbench modes, then an A/B of knob settings on the default bench
 # workload (alternating, two rounds, per-kernel rows in the .err files).
-# Usage: bash scripts/gpu_r4.sh <tag> "<pytest -k expr>" "<microbench modes>" "<variant> ..."
+# Usage: bash scripts/gpu_run.sh <tag> "<pytest -k expr>" "<microbench modes>" "<variant> ..."
 #   variant = a space-free env assignment list joined by commas, e.g. ALCM_AMPAIR=0,ALCM_ACT_MFMA=0 ("-" = defaults)
-tag=${1:-r4}
+tag=${1:-run}
 sel=${2:-"ampblock or bigvgan or bench_batch32"}
 micro=${3:-""}
 variants=${4:-"- ALCM_AMPAIR=1"}

@@ -180,6 +180,43 @@ def bench_wone(B=32):
         print(f"{name}: done", flush=True)
 
 
+def bench_w3var(B=32):
+    """wconv3 SIMD-partner schedules (ALCM_W3_VAR 0 / 1 / 2) on the BigVGAN stage 0-2 AMPBlock shapes as the model
+    runs them (conv1: plane or fp32 out, no residual; conv2: residual, k = 3 accumulate), alternating per shape, plus
+    the conv1 fp16 plane output vs the fp32 output (ALCM_W3_VAR default)"""
+    vars_ = os.environ.get("W3_VARS", "0,1,2").split(",")
+    for C, T in ((768, 2496), (384, 9984), (192, 19968)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        pl = K.operand_planes(x, 2)
+        for k, d in ((11, 5), (7, 3), (3, 1)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            b = torch.randn((C,), device="cuda") * 0.05
+            pw = K.pack_conv_weight(w)
+            tf = 2 * B * T * C * C * k / 1e12
+            res = {v: [] for v in vars_}
+            for rep in range(3):
+                for v in vars_:
+                    os.environ["ALCM_W3_VAR"] = v
+                    _hip.reload_knobs()
+                    res[v].append(timeit(lambda: K.opconv(pl, C, w, b, d, 2, residual=r, packed=pw), reps=5))
+            os.environ.pop("ALCM_W3_VAR")
+            _hip.reload_knobs()
+            line = " | ".join(f"var{v} {min(t):7.3f} ms {tf / min(t) * 1e3:6.0f} TF/s" for v, t in res.items())
+            t32 = timeit(lambda: K.opconv(pl, C, w, b, d, 2, packed=pw), reps=5)
+            t16 = timeit(lambda: K.opconv(pl, C, w, b, d, 2, packed=pw, out_plane=True), reps=5)
+            print(f"w3 C={C:3d} k={k:2d} d={d}: {line} | conv1 fp32 {t32:7.3f} fp16 {t16:7.3f} ms", flush=True)
+        y32 = K.opconv(pl, C, w, b, 1, 2, packed=pw)
+        y16 = K.opconv(pl, C, w, b, 1, 2, packed=pw, out_plane=True)
+        f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        ta32 = timeit(lambda: K.activation1d_op(y32, a, bt, f, f, 2), reps=10)
+        ta16 = timeit(lambda: K.activation1d_op_f16in(y16, a, bt, f, f, 2), reps=10)
+        gb32, gb16 = B * T * C * 6 / 1e9, B * T * C * 4 / 1e9
+        print(f"act C={C:3d}: fp32 in {ta32:7.3f} ms ({gb32 / ta32:5.2f} TB/s) | fp16 in {ta16:7.3f} ms "
+              f"({gb16 / ta16:5.2f} TB/s)", flush=True)
+
+
 def bench_ffn(B=32):
     """DiT Conv1dFeedForward convs (L = 467 tokens): fp32-operand conv_kernel (LayerNorm prologue path) vs the
     wide-layer kernel on operand planes (GEGLU plane epilogue / residual epilogue)"""
@@ -443,4 +480,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"w3var": bench_w3var, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

@@ -730,3 +730,69 @@ def test_activation1d_mfma(K, C, T, monkeypatch):
         monkeypatch.delenv("ALCM_ACT_DEFER")
         _hip.reload_knobs()
     assert torch.equal(got, inl)
+
+
+@pytest.mark.parametrize("C,T,k,dil,grid", [(768, 600, 11, 5, 8), (384, 1100, 7, 3, 0), (192, 1500, 3, 1, 16),
+                                            (192, 257, 11, 5, 0), (192, 37, 3, 1, 0)])
+def test_conv1_fp16_handoff(K, C, T, k, dil, grid, monkeypatch):
+    """The wide-stage AMPBlock conv1 -> Activation1d hand-off (vocoder/bigvgan/models.py:74-79) as an fp16 plane:
+    conv1's out_plane epilogue (wconv3 where its tiles are full, else wconv2) writes fp16(acc + bias) and
+    alcm_activation1d_op_f16in reads it.  Both halves are bit-identical to the fp32 path they replace: the plane equals
+    the fp32 output rounded to fp16, and the activation equals alcm_activation1d_op on the fp32 output (its MFMA FIRs
+    round their input to that same fp16 value)."""
+    from audiolcm_amd import _hip
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B, prec = 2, 2
+    x = _r((B, T, C), 150)
+    w, bias = _r((C, C, k), 151, 0.7 / np.sqrt(C * k)), _r((C,), 152, 0.05)
+    a, bt = _r((C,), 153, 0.3), _r((C,), 154, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    pl = K.operand_planes(dev(x), prec)
+    for w3 in ("1", "0"):  # persistent kernel (grid-capped: several tiles per workgroup), two-workgroup kernel
+        monkeypatch.setenv("ALCM_WCONV3", w3)
+        monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
+        _hip.reload_knobs()
+        try:
+            y32 = K.opconv(pl, C, dev(w), dev(bias), dil, prec)
+            y16 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, out_plane=True)
+            act32 = K.activation1d_op(y32, dev(a), dev(bt), f, f, prec).cpu()
+            act16 = K.activation1d_op_f16in(y16, dev(a), dev(bt), f, f, prec).cpu()
+        finally:
+            monkeypatch.delenv("ALCM_WCONV3")
+            monkeypatch.delenv("ALCM_WCONV3_GRID")
+            _hip.reload_knobs()
+        assert torch.equal(y16.cpu()[0], y32.cpu().half().view(torch.int16)), f"plane != fp16(fp32 out), wconv3={w3}"
+        assert torch.equal(act16, act32), f"activation on the fp16 plane differs, wconv3={w3}"
+
+
+@pytest.mark.parametrize("C,T,k,dil,grid,acc", [(768, 600, 11, 5, 8, True), (384, 1100, 7, 3, 0, False),
+                                                (192, 1500, 3, 1, 16, True), (576, 467, 9, 1, 0, False)])
+def test_wconv3_partner_schedules(K, C, T, k, dil, grid, acc, monkeypatch):
+    """wconv3's SIMD-partner schedules (ALCM_W3_VAR: 0 per-slice s_setprio, 1 static priority for waves 4-7, 2 that
+    plus waves 4-7 staggered by half a step) issue the same MFMAs per accumulator in the same order: bit-identical
+    outputs, fp32 epilogue (residual / accumulate) and fp16 plane epilogue alike."""
+    from audiolcm_amd import _hip
+    B, prec = 2, 2
+    x = _r((B, T, C), 160)
+    w, bias = _r((C, C, k), 161, 0.7 / np.sqrt(C * k)), _r((C,), 162, 0.05)
+    r = dev(_r((B, T, C), 163))
+    pl = K.operand_planes(dev(x), prec)
+    outs = []
+    for var in ("0", "1", "2"):
+        for kk, v in (("ALCM_WCONV3", "1"), ("ALCM_WCONV3_GRID", str(grid)), ("ALCM_W3_VAR", var)):
+            monkeypatch.setenv(kk, v)
+        _hip.reload_knobs()
+        try:
+            o = dev(_r((B, T, C), 164)) if acc else None
+            y = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r, out_scale=0.5, accumulate_into=o).cpu()
+            p = K.opconv(pl, C, dev(w), dev(bias), dil, prec, out_plane=True).cpu()
+            outs.append((y, p))
+        finally:
+            for kk in ("ALCM_WCONV3", "ALCM_WCONV3_GRID", "ALCM_W3_VAR"):
+                monkeypatch.delenv(kk)
+            _hip.reload_knobs()
+    for y, p in outs[1:]:
+        assert torch.equal(y, outs[0][0]) and torch.equal(p, outs[0][1])
+    ref = F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1)
+    ref = (ref + r.cpu()) * 0.5 + (_r((B, T, C), 164) if acc else 0)
+    assert rel_l2(outs[0][0].numpy(), ref.numpy()) < TOL[prec]
