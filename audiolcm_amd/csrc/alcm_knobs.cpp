@@ -59,6 +59,11 @@ static Knobs read_knobs() {
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
   k.w3_var = env_int("ALCM_W3_VAR", 0);
+  k.w3_ablate = env_int("ALCM_W3_ABLATE", 0);
+  k.xp[0] = env_int("ALCM_XP0", 0);
+  k.xp[1] = env_int("ALCM_XP1", 0);
+  k.xp[2] = env_int("ALCM_XP2", 0);
+  k.xp[3] = env_int("ALCM_XP3", 0);
   k.conv1_h16 = env_int("ALCM_CONV1_H16", 1);
   return k;
 }

@@ -348,7 +348,9 @@ __device__ __forceinline__ void w3_wait_barrier() {
 //      first-slice fragments read after the barrier that publishes it) where waves 0-3 run [slice 1 of step g, slice 0
 //      of step g + 1], so one wave's exposed fragment reads meet its partner's MFMA burst.
 // Every variant issues the same MFMAs on the same fragments in the same order per accumulator: bit-identical results.
-template <int PREC, int VAR>
+// ABL (ALCM_W3_ABLATE, timing only, results wrong): 1 no epilogue, 2 no weight DMA in the loop, 4 no window DMA in
+// the loop, 8 no mid-step wait / barrier, 16 no fragment reads in the loop, 32 no MFMAs
+template <int PREC, int VAR, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
@@ -555,14 +557,14 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   //      share; every wave done reading this slot and, at a chunk's last step, this chunk's window.  Loads issued after
   //      weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay in flight
   auto mid_step = [&]() {
-    switch (pieces_last) {
+    if (!(ABL & 8)) switch (pieces_last) {
       case 0: w3_wait_barrier<W3_BPW>(); break;
       case 1: w3_wait_barrier<W3_BPW + 1>(); break;
       case 2: w3_wait_barrier<W3_BPW + 2>(); break;
       default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
     }
     pieces_last = 0;
-    if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
+    if (!(ABL & 4) && tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
       if (tap == 0) win_setup(q + 1);
       for (int j = tap; j < W3_WPW; j += wspread) {
         win_piece(j);
@@ -581,8 +583,8 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
-      if (i == 0) {
+      for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
+      if (i == 0 && !(ABL & 16)) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
 #pragma unroll
@@ -605,14 +607,16 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
         if (i == 0) {
+          if (!(ABL & 16)) {
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+            for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
 #pragma unroll
-          for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+            for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+          }
           // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
-          issue_wt(sl);
+          if (!(ABL & 2)) issue_wt(sl);
         }
       }
       __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
@@ -626,7 +630,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
       mid_step();
 #pragma unroll
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     tap = 0;
     ++q;
     if (++c == nC) {
-      epilogue(ti);
+      if (!(ABL & 1)) epilogue(ti);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -698,7 +702,24 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
     if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, V>), dim3(grid), dim3(512), 0, s, P);
     else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, V>), dim3(grid), dim3(512), 0, s, P);
   };
-  if (var == 1) go(std::integral_constant<int, 1>{});
+  const int abl = knobs().w3_ablate;
+  auto ga = [&](auto ac) {
+    hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1, decltype(ac)::value>), dim3(grid), dim3(512), 0, s, P);
+  };
+  if (abl && a.prec == PREC_F16) {  // timing-only ablations, on the static-priority schedule
+    switch (abl) {
+      case 1: ga(std::integral_constant<int, 1>{}); break;
+      case 7: ga(std::integral_constant<int, 7>{}); break;
+      case 9: ga(std::integral_constant<int, 9>{}); break;
+      case 15: ga(std::integral_constant<int, 15>{}); break;
+      case 17: ga(std::integral_constant<int, 17>{}); break;
+      case 23: ga(std::integral_constant<int, 23>{}); break;
+      case 31: ga(std::integral_constant<int, 31>{}); break;
+      case 33: ga(std::integral_constant<int, 33>{}); break;
+      case 47: ga(std::integral_constant<int, 47>{}); break;
+      default: ga(std::integral_constant<int, 39>{}); break;
+    }
+  } else if (var == 1) go(std::integral_constant<int, 1>{});
   else if (var == 2) go(std::integral_constant<int, 2>{});
   else go(std::integral_constant<int, 0>{});
   if (tok) {

@@ -217,6 +217,32 @@ def bench_w3var(B=32):
               f"({gb16 / ta16:5.2f} TB/s)", flush=True)
 
 
+def bench_w3abl(B=32):
+    """wconv3 timing ablations (ALCM_W3_ABLATE bits: 1 no epilogue, 2 no weight DMA, 4 no window DMA, 8 no mid-step
+    barrier, 16 no fragment reads, 32 no MFMAs; results wrong) on three stage shapes, alternating, best of 3"""
+    abls = os.environ.get("W3_ABLS", "0,1,7,9,15,17,23,31,33,47").split(",")
+    for C, T, k, d in ((768, 2496, 11, 5), (384, 9984, 7, 3), (192, 19968, 3, 1)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        pl = K.operand_planes(x, 2)
+        w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+        b = torch.randn((C,), device="cuda") * 0.05
+        pw = K.pack_conv_weight(w)
+        tf = 2 * B * T * C * C * k / 1e12
+        res = {v: [] for v in abls}
+        for rep in range(3):
+            for v in abls:
+                os.environ["ALCM_W3_ABLATE"] = v
+                os.environ["ALCM_W3_VAR"] = "1"
+                _hip.reload_knobs()
+                res[v].append(timeit(lambda: K.opconv(pl, C, w, b, d, 2, residual=r, packed=pw), reps=5))
+        os.environ.pop("ALCM_W3_ABLATE")
+        os.environ.pop("ALCM_W3_VAR")
+        _hip.reload_knobs()
+        print(f"w3abl C={C:3d} k={k:2d}: " + " | ".join(f"a{v} {min(t) * 1e3:6.1f} us" for v, t in res.items()) +
+              f"  ({tf:.3f} TFLOP)", flush=True)
+
+
 def bench_ffn(B=32):
     """DiT Conv1dFeedForward convs (L = 467 tokens): fp32-operand conv_kernel (LayerNorm prologue path) vs the
     wide-layer kernel on operand planes (GEGLU plane epilogue / residual epilogue)"""
@@ -480,4 +506,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"w3var": bench_w3var, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"w3abl": bench_w3abl, "w3var": bench_w3var, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

