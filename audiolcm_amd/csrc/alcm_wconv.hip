@@ -358,6 +358,10 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches below)
   const int wm = wave >> 1, wn = wave & 1;
   const bool late = VAR == 2 && wave >= 4;
+  // VAR 3: waves 4-7 issue their share of weight step g + 3 in the NEXT step's first slice (into the slot step g read,
+  // free since step g's mid-step barrier) instead of in step g's second slice with waves 0-3, so the two waves of a
+  // SIMD never stall on LDS-DMA issue at the same time; counted waits unchanged (the issue order is the same)
+  const bool hi_dma = VAR == 3 && wave >= 4;
   if (VAR >= 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
@@ -590,6 +594,10 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(q & 1, tap, 1, ii);
       }
+      if (i == 0 && hi_dma && g > 0) {
+        issue_wt(sl == 0 ? 2 : sl - 1);
+        advance_wt();
+      }
     }
     // pin the interleave: all ten reads of the next slice's fragments after the first row's MFMAs, so the newest
     // is 18 MFMAs old when the next slice starts (the compiler's wait there is lgkmcnt(0)); issued before the first
@@ -616,7 +624,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
             for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
           }
           // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
-          if (!(ABL & 2)) issue_wt(sl);
+          if (!(ABL & 2) && !hi_dma) issue_wt(sl);
         }
       }
       __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
@@ -639,7 +647,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
       for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
       issue_wt(sl);
     }
-    advance_wt();
+    if (!hi_dma) advance_wt();
 
     sl = sl1;
     if (!chunk_end) {
@@ -649,7 +657,14 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     tap = 0;
     ++q;
     if (++c == nC) {
-      if (!(ABL & 1)) epilogue(ti);
+      if (!(ABL & 1)) {
+        epilogue(ti);
+      } else {  // (keep the accumulators live: the MFMAs stay in the ablated build)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -709,22 +724,22 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if (abl && a.prec == PREC_F16) {  // timing-only ablations, on the static-priority schedule
     switch (abl) {
       case 1: ga(std::integral_constant<int, 1>{}); break;
+      case 3: ga(std::integral_constant<int, 3>{}); break;
+      case 5: ga(std::integral_constant<int, 5>{}); break;
       case 7: ga(std::integral_constant<int, 7>{}); break;
       case 9: ga(std::integral_constant<int, 9>{}); break;
       case 15: ga(std::integral_constant<int, 15>{}); break;
-      case 17: ga(std::integral_constant<int, 17>{}); break;
-      case 23: ga(std::integral_constant<int, 23>{}); break;
       case 31: ga(std::integral_constant<int, 31>{}); break;
       case 33: ga(std::integral_constant<int, 33>{}); break;
-      case 47: ga(std::integral_constant<int, 47>{}); break;
-      default: ga(std::integral_constant<int, 39>{}); break;
+      default: ga(std::integral_constant<int, 17>{}); break;
     }
   } else if (var == 1) go(std::integral_constant<int, 1>{});
   else if (var == 2) go(std::integral_constant<int, 2>{});
+  else if (var == 3) go(std::integral_constant<int, 3>{});
   else go(std::integral_constant<int, 0>{});
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, %d>", a.prec, var == 1 || var == 2 ? var : 0);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, %d>", a.prec, var >= 1 && var <= 3 ? var : 0);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
