@@ -159,9 +159,6 @@ struct Knobs {
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
   int xp[4] = {0, 0, 0, 0};      // ALCM_XP0..3: scratch switches for an experiment in flight (no default path reads them)
-  int w3_ablate = 0;             // ALCM_W3_ABLATE: wconv3 timing-only ablation bits (alcm_wconv.hip)
-  int w3_var = 0;                // ALCM_W3_VAR: wconv3 SIMD-partner schedule (0 per-slice setprio, 1 static prio for
-                                 // waves 4-7, 2 static prio + waves 4-7 staggered by half a step)
 };
 const Knobs& knobs();
 

@@ -58,8 +58,6 @@ static Knobs read_knobs() {
   k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
-  k.w3_var = env_int("ALCM_W3_VAR", 0);
-  k.w3_ablate = env_int("ALCM_W3_ABLATE", 0);
   k.xp[0] = env_int("ALCM_XP0", 0);
   k.xp[1] = env_int("ALCM_XP1", 0);
   k.xp[2] = env_int("ALCM_XP2", 0);

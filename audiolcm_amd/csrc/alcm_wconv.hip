@@ -340,29 +340,13 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-// VAR (ALCM_W3_VAR, MI355X_MICROARCH.md "Two waves per SIMD"): the two waves sharing a SIMD (w and w + 4) run the same
-// program through one barrier per step, so they reach their MFMA bursts, fragment-read bursts and the barrier together.
-//   0: s_setprio 1 around each slice's MFMA block (round 3);
-//   1: no per-segment flips, one static s_setprio 1 for waves 4-7 (the arbitration losers);
-//   2: 1 + waves 4-7 staggered by half a step: they run [slice 0, slice 1] of a step between two barriers (the slot's
-//      first-slice fragments read after the barrier that publishes it) where waves 0-3 run [slice 1 of step g, slice 0
-//      of step g + 1], so one wave's exposed fragment reads meet its partner's MFMA burst.
-// Every variant issues the same MFMAs on the same fragments in the same order per accumulator: bit-identical results.
-// ABL (ALCM_W3_ABLATE, timing only, results wrong): 1 no epilogue, 2 no weight DMA in the loop, 4 no window DMA in
-// the loop, 8 no mid-step wait / barrier, 16 no fragment reads in the loop, 32 no MFMAs
-template <int PREC, int VAR, int ABL = 0>
+template <int PREC>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches below)
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const bool late = VAR == 2 && wave >= 4;
-  // VAR 3: waves 4-7 issue their share of weight step g + 3 in the NEXT step's first slice (into the slot step g read,
-  // free since step g's mid-step barrier) instead of in step g's second slice with waves 0-3, so the two waves of a
-  // SIMD never stall on LDS-DMA issue at the same time; counted waits unchanged (the issue order is the same)
-  const bool hi_dma = VAR == 3 && wave >= 4;
-  if (VAR >= 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   const int ntiles = P.nwg;
@@ -561,14 +545,14 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   //      share; every wave done reading this slot and, at a chunk's last step, this chunk's window.  Loads issued after
   //      weight step g + 1 (weight step g + 2, and the window issued at the previous mid-step) stay in flight
   auto mid_step = [&]() {
-    if (!(ABL & 8)) switch (pieces_last) {
+    switch (pieces_last) {
       case 0: w3_wait_barrier<W3_BPW>(); break;
       case 1: w3_wait_barrier<W3_BPW + 1>(); break;
       case 2: w3_wait_barrier<W3_BPW + 2>(); break;
       default: w3_wait_barrier<W3_BPW + W3_WPW>(); break;
     }
     pieces_last = 0;
-    if (!(ABL & 4) && tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
+    if (tap < wspread && tap < W3_WPW && q + 1 < nchunks) {
       if (tap == 0) win_setup(q + 1);
       for (int j = tap; j < W3_WPW; j += wspread) {
         win_piece(j);
@@ -578,25 +562,20 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   };
   for (int g = 0; g < total; ++g) {
     const bool chunk_end = tap == K - 1;
-    const bool tile_end = chunk_end && c + 1 == nC;
     const int sl1 = sl == 2 ? 0 : sl + 1;
     const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
     const int ntap = chunk_end ? 0 : tap + 1;
     // ---- slice 0: MFMAs on (aA, bA); slice 1's fragments (this slot, this window) read under them
-    if (VAR == 0) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
-      if (i == 0 && !(ABL & 16)) {
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aA[i], bA[j], acc[i][j]);
+      if (i == 0) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(q & 1, tap, 1, ii);
-      }
-      if (i == 0 && hi_dma && g > 0) {
-        issue_wt(sl == 0 ? 2 : sl - 1);
-        advance_wt();
       }
     }
     // pin the interleave: all ten reads of the next slice's fragments after the first row's MFMAs, so the newest
@@ -605,49 +584,31 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
     __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-    if (VAR == 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
 
-    if (!late) {
-      mid_step();
-      // ---- slice 1: MFMAs on (aB, bB); the next step's slice-0 fragments read under them
-      // (after the last step these re-read resident LDS: harmless)
-      if (VAR == 0) __builtin_amdgcn_s_setprio(1);
+    mid_step();
+    // ---- slice 1: MFMAs on (aB, bB); the next step's slice-0 fragments read under them
+    // (after the last step these re-read resident LDS: harmless)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
-        if (i == 0) {
-          if (!(ABL & 16)) {
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
+      if (i == 0) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
+        for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
 #pragma unroll
-            for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
-          }
-          // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
-          if (!(ABL & 2) && !hi_dma) issue_wt(sl);
-        }
+        for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
+        // weight step g + 3 into the slot this step has finished reading (every wave passed the mid-step barrier)
+        issue_wt(sl);
       }
-      __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
-      __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
-      if (VAR == 0) __builtin_amdgcn_s_setprio(0);
-    } else {
-      // ---- waves 4-7 (VAR 2): slice 1 right behind slice 0 (its fragments are in registers), then the mid-step
-      //      barrier; the next step's slice-0 fragments are read after it (the slot it publishes)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) if constexpr (!(ABL & 32)) acc[i][j] = mfma16<PREC>(aB[i], bB[j], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-      mid_step();
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
-      issue_wt(sl);
     }
-    if (!hi_dma) advance_wt();
+    __builtin_amdgcn_sched_group_barrier(0x8, TN, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+    __builtin_amdgcn_sched_group_barrier(0x10, W3_BPW, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, (TM - 1) * TN, 0);
+    __builtin_amdgcn_s_setprio(0);
+    advance_wt();
 
     sl = sl1;
     if (!chunk_end) {
@@ -657,14 +618,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     tap = 0;
     ++q;
     if (++c == nC) {
-      if (!(ABL & 1)) {
-        epilogue(ti);
-      } else {  // (keep the accumulators live: the MFMAs stay in the ablated build)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-      }
+      epilogue(ti);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -711,35 +665,11 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  const int var = knobs().w3_var;
-  auto go = [&](auto vc) {
-    constexpr int V = decltype(vc)::value;
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, V>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, V>), dim3(grid), dim3(512), 0, s, P);
-  };
-  const int abl = knobs().w3_ablate;
-  auto ga = [&](auto ac) {
-    hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1, decltype(ac)::value>), dim3(grid), dim3(512), 0, s, P);
-  };
-  if (abl && a.prec == PREC_F16) {  // timing-only ablations, on the static-priority schedule
-    switch (abl) {
-      case 1: ga(std::integral_constant<int, 1>{}); break;
-      case 3: ga(std::integral_constant<int, 3>{}); break;
-      case 5: ga(std::integral_constant<int, 5>{}); break;
-      case 7: ga(std::integral_constant<int, 7>{}); break;
-      case 9: ga(std::integral_constant<int, 9>{}); break;
-      case 15: ga(std::integral_constant<int, 15>{}); break;
-      case 31: ga(std::integral_constant<int, 31>{}); break;
-      case 33: ga(std::integral_constant<int, 33>{}); break;
-      default: ga(std::integral_constant<int, 17>{}); break;
-    }
-  } else if (var == 1) go(std::integral_constant<int, 1>{});
-  else if (var == 2) go(std::integral_constant<int, 2>{});
-  else if (var == 3) go(std::integral_constant<int, 3>{});
-  else go(std::integral_constant<int, 0>{});
+  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, %d>", a.prec, var >= 1 && var <= 3 ? var : 0);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);

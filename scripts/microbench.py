@@ -180,67 +180,28 @@ def bench_wone(B=32):
         print(f"{name}: done", flush=True)
 
 
-def bench_w3var(B=32):
-    """wconv3 SIMD-partner schedules (ALCM_W3_VAR 0 / 1 / 2) on the BigVGAN stage 0-2 AMPBlock shapes as the model
-    runs them (conv1: plane or fp32 out, no residual; conv2: residual, k = 3 accumulate), alternating per shape, plus
-    the conv1 fp16 plane output vs the fp32 output (ALCM_W3_VAR default)"""
-    vars_ = os.environ.get("W3_VARS", "0,1,2").split(",")
+def bench_h16(B=32):
+    """the wide stages' conv1 -> Activation1d hand-off: conv1 with an fp32 output + Activation1d of it vs conv1 with
+    an fp16 plane output + the fp16-input Activation1d, per stage shape and conv1 kernel size"""
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
     for C, T in ((768, 2496), (384, 9984), (192, 19968)):
         x = torch.randn((B, T, C), device="cuda")
-        r = torch.randn((B, T, C), device="cuda")
         pl = K.operand_planes(x, 2)
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
         for k, d in ((11, 5), (7, 3), (3, 1)):
             w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
             b = torch.randn((C,), device="cuda") * 0.05
             pw = K.pack_conv_weight(w)
-            tf = 2 * B * T * C * C * k / 1e12
-            res = {v: [] for v in vars_}
-            for rep in range(3):
-                for v in vars_:
-                    os.environ["ALCM_W3_VAR"] = v
-                    _hip.reload_knobs()
-                    res[v].append(timeit(lambda: K.opconv(pl, C, w, b, d, 2, residual=r, packed=pw), reps=5))
-            os.environ.pop("ALCM_W3_VAR")
-            _hip.reload_knobs()
-            line = " | ".join(f"var{v} {min(t):7.3f} ms {tf / min(t) * 1e3:6.0f} TF/s" for v, t in res.items())
             t32 = timeit(lambda: K.opconv(pl, C, w, b, d, 2, packed=pw), reps=5)
             t16 = timeit(lambda: K.opconv(pl, C, w, b, d, 2, packed=pw, out_plane=True), reps=5)
-            print(f"w3 C={C:3d} k={k:2d} d={d}: {line} | conv1 fp32 {t32:7.3f} fp16 {t16:7.3f} ms", flush=True)
+            print(f"conv1 C={C:3d} k={k:2d} d={d}: fp32 out {t32:7.3f} ms | fp16 plane out {t16:7.3f} ms", flush=True)
         y32 = K.opconv(pl, C, w, b, 1, 2, packed=pw)
         y16 = K.opconv(pl, C, w, b, 1, 2, packed=pw, out_plane=True)
-        f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
         ta32 = timeit(lambda: K.activation1d_op(y32, a, bt, f, f, 2), reps=10)
         ta16 = timeit(lambda: K.activation1d_op_f16in(y16, a, bt, f, f, 2), reps=10)
         gb32, gb16 = B * T * C * 6 / 1e9, B * T * C * 4 / 1e9
         print(f"act C={C:3d}: fp32 in {ta32:7.3f} ms ({gb32 / ta32:5.2f} TB/s) | fp16 in {ta16:7.3f} ms "
               f"({gb16 / ta16:5.2f} TB/s)", flush=True)
-
-
-def bench_w3abl(B=32):
-    """wconv3 timing ablations (ALCM_W3_ABLATE bits: 1 no epilogue, 2 no weight DMA, 4 no window DMA, 8 no mid-step
-    barrier, 16 no fragment reads, 32 no MFMAs; results wrong) on three stage shapes, alternating, best of 3"""
-    abls = os.environ.get("W3_ABLS", "0,1,3,5,7,9,15,17,31,33").split(",")
-    for C, T, k, d in ((768, 2496, 11, 5), (384, 9984, 7, 3), (192, 19968, 3, 1)):
-        x = torch.randn((B, T, C), device="cuda")
-        r = torch.randn((B, T, C), device="cuda")
-        pl = K.operand_planes(x, 2)
-        w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
-        b = torch.randn((C,), device="cuda") * 0.05
-        pw = K.pack_conv_weight(w)
-        tf = 2 * B * T * C * C * k / 1e12
-        res = {v: [] for v in abls}
-        for rep in range(3):
-            for v in abls:
-                os.environ["ALCM_W3_ABLATE"] = v
-                os.environ["ALCM_W3_VAR"] = "1"
-                _hip.reload_knobs()
-                res[v].append(timeit(lambda: K.opconv(pl, C, w, b, d, 2, residual=r, packed=pw), reps=5))
-        os.environ.pop("ALCM_W3_ABLATE")
-        os.environ.pop("ALCM_W3_VAR")
-        _hip.reload_knobs()
-        print(f"w3abl C={C:3d} k={k:2d}: " + " | ".join(f"a{v} {min(t) * 1e3:6.1f} us" for v, t in res.items()) +
-              f"  ({tf:.3f} TFLOP)", flush=True)
 
 
 def bench_ffn(B=32):
@@ -506,4 +467,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"w3abl": bench_w3abl, "w3var": bench_w3var, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

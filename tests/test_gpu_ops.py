@@ -766,36 +766,3 @@ def test_conv1_fp16_handoff(K, C, T, k, dil, grid, monkeypatch):
         else:
             assert rel_l2(y16.cpu()[0].view(torch.float16).float().numpy(), y32.cpu().numpy()) < 1e-3
         assert torch.equal(act16, act32), f"activation on the fp16 plane differs, wconv3={w3}"
-
-
-@pytest.mark.parametrize("C,T,k,dil,grid,acc", [(768, 600, 11, 5, 8, True), (384, 1100, 7, 3, 0, False),
-                                                (192, 1500, 3, 1, 16, True), (576, 467, 9, 1, 0, False)])
-def test_wconv3_partner_schedules(K, C, T, k, dil, grid, acc, monkeypatch):
-    """wconv3's SIMD-partner schedules (ALCM_W3_VAR: 0 per-slice s_setprio, 1 static priority for waves 4-7, 2 that
-    plus waves 4-7 staggered by half a step) issue the same MFMAs per accumulator in the same order: bit-identical
-    outputs, fp32 epilogue (residual / accumulate) and fp16 plane epilogue alike."""
-    from audiolcm_amd import _hip
-    B, prec = 2, 2
-    x = _r((B, T, C), 160)
-    w, bias = _r((C, C, k), 161, 0.7 / np.sqrt(C * k)), _r((C,), 162, 0.05)
-    r = dev(_r((B, T, C), 163))
-    pl = K.operand_planes(dev(x), prec)
-    outs = []
-    for var in ("0", "1", "2"):
-        for kk, v in (("ALCM_WCONV3", "1"), ("ALCM_WCONV3_GRID", str(grid)), ("ALCM_W3_VAR", var)):
-            monkeypatch.setenv(kk, v)
-        _hip.reload_knobs()
-        try:
-            o = dev(_r((B, T, C), 164)) if acc else None
-            y = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r, out_scale=0.5, accumulate_into=o).cpu()
-            p = K.opconv(pl, C, dev(w), dev(bias), dil, prec, out_plane=True).cpu()
-            outs.append((y, p))
-        finally:
-            for kk in ("ALCM_WCONV3", "ALCM_WCONV3_GRID", "ALCM_W3_VAR"):
-                monkeypatch.delenv(kk)
-            _hip.reload_knobs()
-    for y, p in outs[1:]:
-        assert torch.equal(y, outs[0][0]) and torch.equal(p, outs[0][1])
-    ref = F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1)
-    ref = (ref + r.cpu()) * 0.5 + (_r((B, T, C), 164) if acc else 0)
-    assert rel_l2(outs[0][0].numpy(), ref.numpy()) < TOL[prec]
