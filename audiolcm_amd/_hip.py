@@ -54,15 +54,6 @@ class OpConvArgs(C.Structure):
                 ("out_stride", C.c_int), ("out_offset", C.c_int), ("out_rows", C.c_int), ("out_plane", vp)]
 
 
-class AmpairArgs(C.Structure):
-    _fields_ = [("x", fp), ("out", fp), ("B", C.c_int), ("T", C.c_int), ("C", C.c_int), ("ksize", C.c_int),
-                ("dil", C.c_int), ("w1", vp), ("w2", vp), ("w_lo_off", i64), ("kpad", C.c_int), ("bias1", fp),
-                ("bias2", fp), ("out_scale", C.c_float), ("accumulate", C.c_int), ("last", C.c_int),
-                ("alpha_exp1", fp), ("inv_beta1", fp), ("alpha_exp2", fp), ("inv_beta2", fp),
-                ("up_filter1", fp), ("down_filter1", fp), ("up_filter2", fp), ("down_filter2", fp),
-                ("prec", C.c_int)]
-
-
 class NamedTensor(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data", vp), ("ndim", C.c_int), ("shape", i64 * 4)]
 
@@ -91,7 +82,6 @@ _SIGS = [
     ("alcm_activation1d_op_f16in", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_opconv_dense", C.c_int, [C.POINTER(OpConvArgs), vp]),
-    ("alcm_ampblock_pair", C.c_int, [C.POINTER(AmpairArgs), vp]),
     ("alcm_flash_attention", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
     ("alcm_layer_norm_plane", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, vp, C.c_int, vp]),
     ("alcm_lcm_step", C.c_int, [fp, fp, fp, C.POINTER(C.c_float), fp, fp, i64, vp]),

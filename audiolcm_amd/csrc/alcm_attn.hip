@@ -275,7 +275,9 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const void* 
   __syncthreads();
 
   const int nqb = (L + 15) / 16, nkt = Lp / FA_KT;
-  // q pre-scaled by scale * log2(e): the scores come out in the log2 domain and p = exp2(s - m) is one v_exp_f32
+  // scores scaled by scale * log2(e) in fp32 after the MFMA (the log2 domain: p = exp2(s - m) is one v_exp_f32); q is
+  // rounded to the operand format unscaled (from a plane: exactly as stored), so the scale costs no second rounding
+  // and no fp16 range (T5's scores are unscaled)
   const float qs = scale * 1.44269504088896341f;
   for (int qb = wave; qb < nqb; qb += FR_THREADS / 64) {
     const int q0 = qb * 16;
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const void* 
         for (int j = 0; j < 8; ++j) {
           const int d = 32 * ks + 8 * g + j;
           const float v = fa_ld<PREC, QH>(qkv, qr + (d < dh ? d : 0));
-          e[j] = fa_cvt<PREC>((qok && d < dh) ? v * qs : 0.f);
+          e[j] = fa_cvt<PREC>((qok && d < dh) ? v : 0.f);
         }
         qf[ks] = __builtin_bit_cast(bf16x8, e);
       }
@@ -326,6 +328,7 @@ __global__ __launch_bounds__(FR_THREADS) void flash_attn_res_kernel(const void* 
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(k0 + 16 * kb + cq) * FR_KS + koff[ks]]);
           s[kb] = mfma16<PREC>(kf, qf[ks], s[kb]);
         }
+        s[kb] *= qs;
       }
       if constexpr (BIAS) {  // additive score bias [head][query][key] (T5's relative positions), into the log2 domain too
         const float* br = bias + ((int64_t)h * bld + min(q0 + cq, L - 1)) * bld;

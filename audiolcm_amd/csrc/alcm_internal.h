@@ -86,13 +86,7 @@ struct ActEpiDev;
 int tconv(const alcm_opconv_args& a, const unsigned short* wd, int64_t wd_lo, int kd, const ActEpiDev* act,
           double flops, double bytes, hipStream_t s);
 
-// fused AMPBlock1 half-layer pair of the narrow stages (alcm_ampair.hip): act1 -> conv1 -> act2 -> conv2 + x
-bool ampair_supported(int prec, int C, int ksize, int dil);
 struct Taps12O;
-int ampair(const float* x, float* out, int B, int T, int C, int ksize, int dil, const unsigned short* w1,
-           const unsigned short* w2, int64_t w_lo, int kd, const float* b1, const float* b2, float out_scale,
-           int accumulate, bool last, const float* ae1, const float* ib1, const Taps12O& f1, const float* ae2,
-           const float* ib2, const Taps12O& f2, int prec, hipStream_t s);
 
 // BigVGAN stride-2 / kernel-4 upsampler, both phases in one split-precision pass (alcm_ups.hip)
 bool ups2_supported(int cin, int cout, int cpad, int rate, int taps);
@@ -149,11 +143,6 @@ struct Knobs {
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
                                  // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv
   int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
-  int ampair = 0;                // ALCM_AMPAIR (opt-in): BigVGAN stages 3-5 as fused AMPBlock half-layer pairs (alcm_ampair.hip),
-                                 // 0 = one launch per Activation1d / conv (tconv)
-  int ampair_grid = 0;           // ALCM_AMPAIR_GRID: cap on the fused pair kernel's persistent workgroups (tests)
-  int ampair_ablate = 0;         // ALCM_AMPAIR_ABLATE: timing-only ablation bits of the fused pair kernel
-  int ampair_nw = 0;             // ALCM_AMPAIR_NW: fused pair waves per workgroup (0 by shape, 4 = two per CU, 8)
   int act_defer = 1;             // ALCM_ACT_DEFER: act_mfma issues a tile's plane stores one tile late, before the next
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)

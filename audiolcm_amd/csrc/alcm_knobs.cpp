@@ -52,10 +52,6 @@ static Knobs read_knobs() {
   k.text_flash = env_int("ALCM_TEXT_FLASH", 1);
   k.qkv_plane = env_int("ALCM_QKV_PLANE", 1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
-  k.ampair = env_int("ALCM_AMPAIR", 0);  // opt-in until it beats the unfused chain
-  k.ampair_grid = env_int("ALCM_AMPAIR_GRID", 0);
-  k.ampair_ablate = env_int("ALCM_AMPAIR_ABLATE", 0);
-  k.ampair_nw = env_int("ALCM_AMPAIR_NW", 0);
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
   k.xp[0] = env_int("ALCM_XP0", 0);

@@ -863,7 +863,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       g.w = wq.w.p; g.w_lo_off = wq.w.lo; g.kpad = wq.w.kpad; g.N = wq.w.rows;
       g.bias = wq.b; g.out = w.qkv; g.out_scale = 1.f; g.prec = pff;
       // q / k / v as an operand plane (attention rounds them to pff anyway): half the bytes written and staged
-      const bool qp = knobs().qkv_plane && wq.w.rows % 4 == 0 && L <= 512;
+      const bool qp = knobs().qkv_plane && wq.w.rows % 4 == 0 && L <= 512 && !knobs().attn_tiled;
       if (qp) {
         g.out = nullptr;
         g.out_plane = w.qkv;
@@ -1351,36 +1351,6 @@ static bool stage_tconv(const StageW& S, int prec) {
   return true;
 }
 
-// the narrow stages' AMPBlock half-layer pairs as one fused launch each (alcm_ampair.hip): every pair of the stage
-// or none
-static bool stage_ampair(const StageW& S, int prec) {
-  if (!knobs().ampair || S.rb.empty() || !S.rb[0].c1[0].dw.p) return false;  // ALCM_AMPAIR=1: opt-in
-  for (const AmpW& A : S.rb)
-    for (size_t l = 0; l < A.dil.size(); ++l)
-      if (!ampair_supported(prec, S.cout, A.k, A.dil[l]) || A.act.size() < 2 * A.dil.size()) return false;
-  return true;
-}
-
-// x_next = x + c2(a2(c1(a1(x)))) of half-layer pair l of resblock A (models.py:72-81); last: the resblock's output
-// times out_scale added into (accumulate) or written to `out` (the stage mean, models.py:190-199)
-static int amp_pair(hipStream_t s, const AmpW& A, size_t l, const float* x, float* out, int B, int T, int C,
-                    float out_scale, int accumulate, bool last, int prec) {
-  const ActW& a1 = A.act[2 * l];
-  const ActW& a2 = A.act[2 * l + 1];
-  Taps12O f1, f2;
-  for (int k = 0; k < 12; ++k) {
-    f1.up[k] = 2.0f * a1.fup[k];  // UpSample1d's ratio-2 gain folded in (resample.py:30)
-    f1.dn[k] = a1.fdn[k];
-    f2.up[k] = 2.0f * a2.fup[k];
-    f2.dn[k] = a2.fdn[k];
-  }
-  const Packed& d1 = A.c1[l].dw;
-  const Packed& d2 = A.c2[l].dw;
-  if (d1.lo != d2.lo || d1.kpad != d2.kpad) return set_error(ALCM_E_INVALID, "amp_pair: weight layouts differ");
-  return ampair(x, out, B, T, C, A.k, A.dil[l], d1.p + 2 * d1.lo, d2.p + 2 * d2.lo, d1.lo, d1.kpad, A.c1[l].b,
-                A.c2[l].b, out_scale, accumulate, last, a1.aexp, a1.ibeta, f1, a2.aexp, a2.ibeta, f2, prec, s);
-}
-
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
                       float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
                       const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false,
@@ -1502,13 +1472,12 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const float inv = 1.0f / (float)S.rb.size();
     const bool fuse = opconv_act_supported(pamp, S.cout, round_up(S.cout, 32));
     const bool dense = fuse && stage_tconv(S, pamp);
-    const bool pair = dense && stage_ampair(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
     // the wide stages' conv1 -> Activation1d hand-off as an fp16 plane (ALCM_CONV1_H16=0: fp32, the A/B reference)
     const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
     // the three chains' first Activation1d in one pass over u (their own planes, same taps; ALCM_ACT3=0: one per chain)
-    bool act3 = conc && fuse && !pair && S.rb.size() == 3 && knobs().act3 &&
+    bool act3 = conc && fuse && S.rb.size() == 3 && knobs().act3 &&
                 !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
     for (size_t j = 1; act3 && j < S.rb.size(); ++j)
       act3 = !std::memcmp(S.rb[j].act[0].fup, S.rb[0].act[0].fup, sizeof(S.rb[0].act[0].fup)) &&
@@ -1534,14 +1503,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
         const bool last = l + 1 == A.dil.size();
         // the mean over resblocks accumulates into x: the chains' last convs run in order (j-1 before j)
         if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, ax->ev[j], 0));
-        if (pair) {
-          ALCM_TRY(amp_pair(sj, A, l, cur, last ? x : nxt, B, To, S.cout, last ? inv : 1.f, last && j > 0, last,
-                            pamp));
-          if (!last) {
-            cur = nxt;
-            nxt = nxt == cb.rb ? cb.t : cb.rb;
-          }
-        } else if (fuse) {
+        if (fuse) {
           if (l == 0 && !act3) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
                               &A.act[2 * l + 1], cb.pl2, dense));
@@ -1806,7 +1768,7 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   const bool planes = (pl == PREC_F16 || pl == PREC_BF16) && H % 64 == 0 && D % 64 == 0 && TI % 64 == 0 &&
                       X.b_inter % 64 == 0 && X.t_ff % 64 == 0;
   // attention of both towers in the fused kernel (ALCM_TEXT_FLASH=0: score GEMM + softmax + PV GEMM)
-  const bool tflash = planes && knobs().text_flash && L <= 512 && H / X.b_heads <= 72 && X.t_dkv <= 72 &&
+  const bool tflash = planes && knobs().text_flash && !knobs().attn_tiled && L <= 512 && H / X.b_heads <= 72 && X.t_dkv <= 72 &&
                       (H / X.b_heads) % 4 == 0 && X.t_dkv % 4 == 0;
   for (const BertLayerW& Ly : X.bl) {
     if (planes) {

@@ -721,6 +721,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   // N % 96: whole tiles; else (N % 4, not strided / GEGLU) 128 x 192 tiles with a partial last one (the T5 wi, N = 5632)
   const bool ragged = a.N % 96 != 0;
   if (ragged && (a.N % 4 || strided || a.geglu_plane)) return 0;
+  // (only where the padded last tile wastes <= 25 % of the N tiles' columns: the text encoders' T5 wi / o, N = 5632 /
+  // 1024; small ragged N stay on opconv_kernel's narrower tiles)
+  if (ragged && 4 * (round_up(a.N, 192) - a.N) > round_up(a.N, 192)) return 0;
   if (!a.geglu_plane && !strided && !a.out_plane && (int64_t)a.B * a.T < 1024) return 0;  // small problems: opconv_kernel's
                                                                                      // 128-row tiles fill the chip better
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };

@@ -436,42 +436,6 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     return out
 
 
-def ampblock_pair(x_cl: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-                  dilation: int, act1: tuple, act2: tuple, prec: int, out_scale: float = 1.0,
-                  accumulate_into: Optional[torch.Tensor] = None, last: bool = False) -> torch.Tensor:
-    """One AMPBlock1 half-layer pair (vocoder/bigvgan/models.py:72-81) in one launch (alcm_ampblock_pair):
-    x + conv2_{k,1}(Act2(conv1_{k,dilation}(Act1(x)))) on channels-last (B, T, C) fp32; act = (alpha, beta,
-    up_filter, down_filter).  last=True: (that) * out_scale, added into `accumulate_into` when given (the resblock
-    mean), else returned."""
-    B, T, Cc = x_cl.shape
-    N, cin, k = w1.shape
-    assert N == cin == Cc and w2.shape == w1.shape
-    x_cl = x_cl.contiguous()
-    p1, p2 = pack_conv_weight(w1), pack_conv_weight(w2)
-    keep = []
-
-    def act(a):
-        alpha, beta, fu, fd = a
-        ae, ib = snake_params(alpha, beta)
-        ae, ib = ae.contiguous(), ib.contiguous()
-        fu = fu.detach().reshape(-1).float().cpu().contiguous()
-        fd = fd.detach().reshape(-1).float().cpu().contiguous()
-        keep.extend([ae, ib, fu, fd])
-        return ptr(ae), ptr(ib), fu.data_ptr(), fd.data_ptr()
-    a = _hip.AmpairArgs()
-    out = accumulate_into if accumulate_into is not None else torch.empty_like(x_cl)
-    a.x, a.out, a.B, a.T, a.C, a.ksize, a.dil = ptr(x_cl), ptr(out), B, T, Cc, k, dilation
-    a.w1, a.w2, a.w_lo_off, a.kpad = ptr(p1.data), ptr(p2.data), p1.lo_off, p1.kpad
-    a.bias1, a.bias2 = ptr(b1.contiguous()), ptr(b2.contiguous())
-    a.out_scale, a.accumulate, a.last = out_scale, int(accumulate_into is not None), int(last)
-    a.alpha_exp1, a.inv_beta1, a.up_filter1, a.down_filter1 = act(act1)
-    a.alpha_exp2, a.inv_beta2, a.up_filter2, a.down_filter2 = act(act2)
-    a.prec = int(prec)
-    check(lib().alcm_ampblock_pair(C.byref(a), stream_handle()), "ampblock_pair")
-    del keep
-    return out
-
-
 def flash_attention(qkv: torch.Tensor, heads: int, prec: int) -> torch.Tensor:
     """(B, L, 3H) fp32 [q | k | v] rows -> (B, L, H) multi-head softmax(q k^T / sqrt(dh)) v (fused kernel)."""
     B, L, H3 = qkv.shape

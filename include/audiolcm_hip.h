@@ -171,6 +171,8 @@ int alcm_activation1d_op_f16in(const void* x16, void* y, int B, int T, int C, in
  * packed by alcm_pack_conv_weight with cpad = Cp; epilogue as alcm_gemm: v = acc + bias[n];
  * v = act(v); v += res; v *= out_scale; if accumulate v += out.  prec: BF16 / SPLIT / F16 / F16W2
  * (must match the planes a holds); C = real input channels (cost accounting). */
+/* Zero-initialise the whole struct (memset / `= {0}`) before setting fields: optional trailing fields (act_*, geglu_plane,
+ * out_stride / out_offset / out_rows, out_plane) are read as "off" only when zero, and later versions append more. */
 typedef struct alcm_opconv_args {
   const void* a;
   int64_t a_lo_off;
@@ -222,38 +224,6 @@ int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
  * Activation1d writes only channels < N of its planes.  Epilogues: act (conv1), res + out + act (conv2), res + out
  * with out_scale and accumulate, no act (a resblock's last conv2).  ALCM_E_INVALID for anything else. */
 int alcm_opconv_dense(const alcm_opconv_args* args, alcm_stream_t stream);
-/* alcm_ampblock_pair: one AMPBlock1 half-layer pair of BigVGAN stages 3-5 in one launch (vocoder/bigvgan/models.py:
- * 72-81: xt = a1(x); xt = c1(xt); xt = a2(xt); xt = c2(xt); x = xt + x), replacing an Activation1d and two
- * alcm_opconv_dense calls: out = x + conv2_{k,1}(Act2(conv1_{k,dil}(Act1(x)))) with same-length zero padding, or,
- * with last != 0, out = (that) * out_scale (+ out if accumulate) — a resblock's last pair adding its share of the
- * stage mean (models.py:190-199).  x, out: (B,T,C) fp32 channels-last DEVICE, out must not overlap x.  w1 / w2 packed
- * by alcm_pack_conv_weight with cpad = C (dense K = tap*C + c, kpad = round_up(ksize*C, 32), planes w_lo_off elements
- * apart).  Activations as alcm_opconv's fused epilogue: alpha_exp / inv_beta DEVICE arrays of C, the 12-tap filters
- * HOST arrays.  C = 24 / 48 with prec F16W2, C = 96 with F16; ksize 3 / 7 / 11; 1 <= dil <= 5.  Bit-identical
- * to alcm_activation1d_op -> alcm_opconv_dense (conv1 + Activation1d) -> alcm_opconv_dense (conv2 + residual). */
-typedef struct alcm_ampair_args {
-  const float* x;
-  float* out;
-  int B, T, C, ksize, dil;
-  const void* w1;
-  const void* w2;
-  int64_t w_lo_off;
-  int kpad;
-  const float* bias1;
-  const float* bias2;
-  float out_scale;
-  int accumulate, last;
-  const float* alpha_exp1;
-  const float* inv_beta1;
-  const float* alpha_exp2;
-  const float* inv_beta2;
-  const float* up_filter1;
-  const float* down_filter1;
-  const float* up_filter2;
-  const float* down_filter2;
-  int prec;
-} alcm_ampair_args;
-int alcm_ampblock_pair(const alcm_ampair_args* args, alcm_stream_t stream);
 
 /* alcm_flash_attention: multi-head self-attention of the DiT (CrossAttention with context = x,
  * ldm/modules/new_attention.py:89-130, the q/k/v projections already applied):

@@ -2,11 +2,11 @@
 # GPU call: selected GPU tests, optional microbench modes, then an A/B of knob settings on the default bench
 # workload (alternating, two rounds, per-kernel rows in the .err files).
 # Usage: bash scripts/gpu_run.sh <tag> "<pytest -k expr>" "<microbench modes>" "<variant> ..."
-#   variant = a space-free env assignment list joined by commas, e.g. ALCM_AMPAIR=0,ALCM_ACT_MFMA=0 ("-" = defaults)
+#   variant = a space-free env assignment list joined by commas, e.g. ALCM_CONV1_H16=0,ALCM_ACT_MFMA=0 ("-" = defaults)
 tag=${1:-run}
-sel=${2:-"ampblock or bigvgan or bench_batch32"}
+sel=${2:-"bigvgan or bench_batch32"}
 micro=${3:-""}
-variants=${4:-"- ALCM_AMPAIR=1"}
+variants=${4:-"-"}
 out=gpurun_out/$tag; mkdir -p $out
 if [ "$sel" != "none" ]; then
   # no -x: test failures (exit 1) are reported and the measurements still run; anything else (a crash, a time
@@ -15,7 +15,7 @@ if [ "$sel" != "none" ]; then
     > $out/tests.log 2>&1
   rc=$?
   echo "TESTS EXIT $rc" >> $out/tests.log
-  grep -E "FAILED|ERROR|passed|failed|ampair C" $out/tests.log | tail -60
+  grep -E "FAILED|ERROR|passed|failed" $out/tests.log | tail -60
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
 for m in $micro; do

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Dev tool: per-kernel VGPR / spill / LDS table of one HIP source (hipcc -Rpass-analysis=kernel-resource-usage).
-Usage: python scripts/kres.py audiolcm_amd/csrc/alcm_ampair.hip [name filter]"""
+Usage: python scripts/kres.py audiolcm_amd/csrc/alcm_wconv.hip [name filter]"""
 import os
 import re
 import subprocess

@@ -365,40 +365,6 @@ def bench_tail1(B=32):
     torch.cuda.synchronize()
 
 
-def bench_ampair(B=32):
-    """Fused AMPBlock pair (alcm_ampair.hip) on the BigVGAN tail shapes vs the unfused chain it replaces (standalone
-    Activation1d -> dense conv1 + fused Activation1d -> dense conv2 + residual), with ablations
-    (ALCM_AMPAIR_ABLATE: 1 no act1, 2 no act2, 4 no MFMAs, 8 no stores)."""
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    spin()
-    for C, T, prec in ((96, 39936, 2), (48, 79872, 3), (24, 159744, 3)):
-        for k, d in ((11, 5), (3, 1)):
-            g = torch.Generator().manual_seed(0)
-            x = torch.randn((B, T, C), generator=g).cuda()
-            w1 = (torch.randn((C, C, k), generator=g) / (C * k) ** 0.5).cuda()
-            w2 = (torch.randn((C, C, k), generator=g) / (C * k) ** 0.5).cuda()
-            b1 = (0.05 * torch.randn((C,), generator=g)).cuda()
-            b2 = (0.05 * torch.randn((C,), generator=g)).cuda()
-            a1 = ((0.3 * torch.randn((C,), generator=g)).cuda(), (0.3 * torch.randn((C,), generator=g)).cuda(), f, f)
-            a2 = ((0.3 * torch.randn((C,), generator=g)).cuda(), (0.3 * torch.randn((C,), generator=g)).cuda(), f, f)
-
-            def chain():
-                pl1 = K.activation1d_op(x, *a1, prec)
-                _, pl2 = K.opconv(pl1, C, w1, b1, d, prec, act=a2, fp32_out=False, dense=True)
-                K.opconv(pl2, C, w2, b2, 1, prec, residual=x, dense=True)
-            res = [f"chain {timeit(chain):7.3f}"]
-            for nw in (("0", "4") if C != 96 else ("0",)):
-                os.environ["ALCM_AMPAIR_NW"] = nw
-                for ab in ("0", "3", "4", "7"):
-                    os.environ["ALCM_AMPAIR_ABLATE"] = ab
-                    _hip.reload_knobs()
-                    res.append(f"nw{nw}ab{ab} {timeit(lambda: K.ampblock_pair(x, w1, b1, w2, b2, d, a1, a2, prec)):7.3f}")
-            os.environ.pop("ALCM_AMPAIR_ABLATE")
-            os.environ.pop("ALCM_AMPAIR_NW")
-            _hip.reload_knobs()
-            print(f"ampair C{C} k{k} d{d}: " + " ".join(res) + " ms", flush=True)
-
-
 def bench_text(B=32):
     """Text encoders (BERT-base + CLAP Projection + T5-v1.1-large, mixed policy) at the bench batch: per-kernel rows of
     one instrumented call (ALCM_PROF_SHAPES=1 splits them per shape) and the wall time per call."""
@@ -467,4 +433,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "ampair": bench_ampair, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()

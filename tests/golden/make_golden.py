@@ -158,22 +158,24 @@ def main():
         if "base" in groups:
             base_fixtures(lcm, smp, voc, scheduling_lcm, orig, meta, Activation1d, SnakeBeta)
         if "c2" in groups:
-            # ---- config 2, last prompt of the bench batch: seed 31, context seed 1031 (bench.py ids 0..31) ----
-            xT, noise = recipe.prompt_noise([31], 2, 20, 312)
-            c = recipe.synthetic_context(1, seed0=1031)
-            calls = {"i": 0}
+            # ---- config 2, single prompts spread over the bench batch: prompt id p has seed p and context seed
+            # 1000 + p (bench.py ids 0..31); 31 is the last one, 7 / 15 / 23 the interior ones ----
+            for pid in (7, 15, 23, 31):
+                xT, noise = recipe.prompt_noise([pid], 2, 20, 312)
+                c = recipe.synthetic_context(1, seed0=1000 + pid)
+                calls = {"i": 0}
 
-            def fake_randn31(*a, **k):
-                calls["i"] += 1
-                return noise[calls["i"] - 1].clone()
-            scheduling_lcm.torch.randn = fake_randn31
-            try:
-                z, _ = smp.sample(S=2, conditioning=c, batch_size=1, shape=[20, 312], verbose=False,
-                                  guidance_scale=5, original_inference_steps=50, x_T=xT.clone())
-            finally:
-                scheduling_lcm.torch.randn = orig
-            mel = lcm.decode_first_stage(z)
-            save("e2e_S2_prompt31.npz", x_T=xT, noise=noise, latent=z, mel=mel, wav=voc(mel).squeeze(1))
+                def fake_randn_p(*a, **k):
+                    calls["i"] += 1
+                    return noise[calls["i"] - 1].clone()
+                scheduling_lcm.torch.randn = fake_randn_p
+                try:
+                    z, _ = smp.sample(S=2, conditioning=c, batch_size=1, shape=[20, 312], verbose=False,
+                                      guidance_scale=5, original_inference_steps=50, x_T=xT.clone())
+                finally:
+                    scheduling_lcm.torch.randn = orig
+                mel = lcm.decode_first_stage(z)
+                save(f"e2e_S2_prompt{pid}.npz", x_T=xT, noise=noise, latent=z, mel=mel, wav=voc(mel).squeeze(1))
         if "enc" in groups:
             # ---- audio -> latent direction: Encoder1D + quant_conv of the reference
             # AutoencoderKL, and the reference MelNet (NAT_mel.py) with librosa's filterbank restated

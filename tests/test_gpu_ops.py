@@ -508,6 +508,55 @@ def test_lin_plane_k1(K, C, N, T, mode, prec, monkeypatch):
     assert all(torch.equal(outs[v], outs["0"]) for v in ("1", "2", "-1"))
 
 
+@pytest.mark.parametrize("C,N,mode", [(1024, 1024, "res"), (1024, 5632, "plain"), (768, 3072, "gelu"),
+                                      (576, 576, "res")])
+@pytest.mark.parametrize("lin1", ["0", "-1"])
+def test_k1_text_shapes_concurrent_streams(K, C, N, mode, lin1, monkeypatch):
+    """The k = 1 convs at the benchmarked text-encoder batch (B = 32 x 77 tokens = 2464 rows; T5 o / wi with ragged
+    N = 1024 / 5632, the BERT intermediate with its GELU epilogue, the DiT to_out shape), on the two-workgroup wide conv
+    (ALCM_LIN1=0: its single-buffered window is re-staged at every step behind a vmcnt(0) + barrier) and on the default
+    routing (lin_plane_kernel where eligible).  The round-1 wconv_kernel raced here: its K = 1 chunks read a window
+    whose DMA the step's counted wait left in flight.  Two launches on concurrent streams, repeated,
+    must equal the single-stream result bit for bit and match F.conv1d."""
+    from audiolcm_amd import _hip
+    B, T, prec = 32, 77, 2
+    xs = [_r((B, T, C), 190 + i) for i in range(2)]
+    w, bias = _r((N, C, 1), 192, 1.0 / np.sqrt(C)), _r((N,), 193, 0.05)
+    r = dev(_r((B, T, N), 194))
+    pls = [K.operand_planes(dev(x), prec) for x in xs]
+    wd, bd = dev(w), dev(bias)
+    pw = K.pack_conv_weight(wd)
+
+    def run(pl):
+        if mode == "res":
+            return K.opconv(pl, C, wd, bd, 1, prec, residual=r, out_scale=0.5, packed=pw)
+        return K.opconv(pl, C, wd, bd, 1, prec, packed=pw, out_act=2 if mode == "gelu" else 0)
+    monkeypatch.setenv("ALCM_LIN1", lin1)
+    _hip.reload_knobs()
+    try:
+        single = [run(pl).cpu() for pl in pls]
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for _ in range(4):
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s1):
+                y1 = run(pls[0])
+            with torch.cuda.stream(s2):
+                y2 = run(pls[1])
+            torch.cuda.synchronize()
+            assert torch.equal(y1.cpu(), single[0]) and torch.equal(y2.cpu(), single[1])
+    finally:
+        monkeypatch.delenv("ALCM_LIN1")
+        _hip.reload_knobs()
+    for x, y in zip(xs, single):
+        ref = F.conv1d(x.permute(0, 2, 1), w, bias).permute(0, 2, 1)
+        if mode == "gelu":
+            ref = F.gelu(ref)
+        if mode == "res":
+            ref = (ref + r.cpu()) * 0.5
+        assert torch.isfinite(y).all()
+        assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+
+
 @pytest.mark.parametrize("Cin,N,T,rate,prec", [(768, 384, 300, 4, 2), (384, 192, 700, 2, 0), (1536, 768, 40, 4, 2),
                                                  (192, 96, 900, 2, 2), (96, 48, 333, 2, 0)])
 def test_opconv_strided_convtranspose(K, Cin, N, T, rate, prec):
@@ -642,58 +691,6 @@ def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_ref)
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_d, dense=True)
         assert rel_l2(o_d.cpu().numpy(), o_ref.cpu().numpy()) < 1e-5
-
-
-@pytest.mark.parametrize("C,T,k,dil,prec,grid", [(24, 1000, 11, 5, 3, 0), (48, 700, 7, 3, 3, 0), (96, 500, 3, 1, 2, 0),
-                                                 (96, 333, 11, 5, 2, 0), (96, 600, 7, 3, 2, 0), (24, 37, 3, 1, 3, 0),
-                                                 (48, 2000, 11, 5, 3, 8), (24, 5000, 7, 1, 3, 8), (96, 1300, 11, 1, 2, 16)])
-@pytest.mark.parametrize("mode", ["state", "last"])
-@pytest.mark.parametrize("nw", [0, 4])
-def test_ampblock_pair_fused(K, C, T, k, dil, prec, grid, mode, nw, monkeypatch):
-    """One AMPBlock1 half-layer pair in one launch (alcm_ampblock_pair, vocoder/bigvgan/models.py:72-81) == the unfused
-    chain it replaces: Activation1d -> operand planes, dense conv1 with the fused Activation1d epilogue, dense conv2 +
-    residual (alcm_opconv_dense) — the same dense K slices, MFMA lanes and Activation1d chains, so bit-identical — incl.
-    the sequence ends (replicate / zero padding), partial last tiles and several tiles per workgroup
-    (ALCM_AMPAIR_GRID); 'last' = a resblock's last pair: (x + ...) * out_scale added into the stage accumulator.
-    nw = 0: the default weight modes (C = 24 resident, C = 48 swapped, C = 96 5-slot ring); nw = 4: the 3-slot-ring
-    two-workgroups-per-CU variants (C = 24 / 48)."""
-    from audiolcm_amd import _hip
-    from audiolcm_amd.recipe import kaiser_sinc_filter1d
-    B = 2
-    x = dev(_r((B, T, C), 130))
-    w1, b1 = dev(_r((C, C, k), 131, 0.7 / np.sqrt(C * k))), dev(_r((C,), 132, 0.05))
-    w2, b2 = dev(_r((C, C, k), 133, 0.7 / np.sqrt(C * k))), dev(_r((C,), 134, 0.05))
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    act1 = (dev(_r((C,), 135, 0.3)), dev(_r((C,), 136, 0.3)), f, f)
-    act2 = (dev(_r((C,), 137, 0.3)), dev(_r((C,), 138, 0.3)), f, f)
-    pl1 = K.activation1d_op(x, *act1, prec)
-    _, pl2 = K.opconv(pl1, C, w1, b1, dil, prec, act=act2, fp32_out=False, dense=True)
-    if mode == "state":
-        ref = K.opconv(pl2, C, w2, b2, 1, prec, residual=x, dense=True)
-    else:
-        ref = dev(_r((B, T, C), 139))
-        K.opconv(pl2, C, w2, b2, 1, prec, residual=x, out_scale=1 / 3, accumulate_into=ref, dense=True)
-    if nw and C == 96:
-        pytest.skip("C = 96 has one geometry")
-    env = {k_: str(v) for k_, v in (("ALCM_AMPAIR_GRID", grid), ("ALCM_AMPAIR_NW", nw)) if v}
-    for k_, v in env.items():
-        monkeypatch.setenv(k_, v)
-    _hip.reload_knobs()
-    try:
-        if mode == "state":
-            y = K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec)
-        else:
-            y = dev(_r((B, T, C), 139))
-            K.ampblock_pair(x, w1, b1, w2, b2, dil, act1, act2, prec, out_scale=1 / 3, accumulate_into=y, last=True)
-    finally:
-        for k_ in env:
-            monkeypatch.delenv(k_)
-        _hip.reload_knobs()
-    y, ref = y.cpu(), ref.cpu()
-    assert torch.isfinite(y).all()
-    d = (y - ref).abs().max().item()
-    print(f"ampair C{C} T{T} k{k} d{dil} {mode}: max |diff| {d:.3e} equal {torch.equal(y, ref)}")
-    assert rel_l2(y.numpy(), ref.numpy()) < 2e-6
 
 
 @pytest.mark.parametrize("C,T", [(192, 37), (384, 300), (768, 2496), (192, 1000)])
