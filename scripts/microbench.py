@@ -204,6 +204,46 @@ def bench_h16(B=32):
               f"({gb16 / ta16:5.2f} TB/s)", flush=True)
 
 
+def bench_xp(B=32):
+    """A/B of a scratch switch (XP_NAME=ALCM_XP0 by default, values XP_VALS) on the BigVGAN stage 0-2 AMPBlock conv2
+    shapes as the model runs them (residual; the k = 3 resblock's last conv2 also accumulates), alternating, best of 3,
+    with the outputs compared bit for bit"""
+    name, vals = os.environ.get("XP_NAME", "ALCM_XP0"), os.environ.get("XP_VALS", "0,1").split(",")
+    for C, T in ((768, 2496), (384, 9984), (192, 19968)):
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        acc0 = torch.randn((B, T, C), device="cuda")
+        pl = K.operand_planes(x, 2)
+        for k, accum in ((11, False), (7, False), (3, False), (3, True)):
+            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+            b = torch.randn((C,), device="cuda") * 0.05
+            pw = K.pack_conv_weight(w)
+            tf = 2 * B * T * C * C * k / 1e12
+            res, outs = {v: [] for v in vals}, {}
+            for rep in range(3):
+                for v in vals:
+                    os.environ[name] = v
+                    _hip.reload_knobs()
+                    if accum:
+                        o = acc0.clone()
+                        fn = lambda: K.opconv(pl, C, w, b, 1, 2, residual=r, packed=pw, out_scale=1 / 3, accumulate_into=o)
+                    else:
+                        fn = lambda: K.opconv(pl, C, w, b, 1, 2, residual=r, packed=pw)
+                    res[v].append(timeit(fn, reps=5))
+                    if rep == 0:
+                        if accum:
+                            o = acc0.clone()
+                            K.opconv(pl, C, w, b, 1, 2, residual=r, packed=pw, out_scale=1 / 3, accumulate_into=o)
+                            outs[v] = o
+                        else:
+                            outs[v] = K.opconv(pl, C, w, b, 1, 2, residual=r, packed=pw)
+            os.environ.pop(name)
+            _hip.reload_knobs()
+            same = all(torch.equal(outs[vals[0]], outs[v]) for v in vals[1:])
+            line = " | ".join(f"{v}: {min(t):7.3f} ms {tf / min(t) * 1e3:6.0f} TF/s" for v, t in res.items())
+            print(f"conv2 C={C:3d} k={k:2d}{' acc' if accum else '    '}: {line} | identical {same}", flush=True)
+
+
 def bench_ffn(B=32):
     """DiT Conv1dFeedForward convs (L = 467 tokens): fp32-operand conv_kernel (LayerNorm prologue path) vs the
     wide-layer kernel on operand planes (GEGLU plane epilogue / residual epilogue)"""
@@ -433,4 +473,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
