@@ -340,7 +340,7 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-template <int PREC, bool OLDEPI = false>
+template <int PREC>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
@@ -497,7 +497,6 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         }
       return;
     }
-    if constexpr (OLDEPI) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       float rv[4][TN], pv[4][TN];
@@ -521,49 +520,6 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         for (int j = 0; j < TN; ++j)
           P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
       }
-    }
-    return;
-    } else {
-    // fp32: every load / store a raw buffer access at a fixed count — rows past the clip's end fall outside the tile's
-    // buffer range (dropped stores, zero loads) instead of branching — and the residual / accumulate loads of
-    // accumulator-row pair h + 1 issued before the stores of pair h, so each pair waits for its own loads only (not, as
-    // in one load-then-store loop, for every store issued before them too)
-    const int64_t r0 = (int64_t)b * P.T + t0;
-    const int nrec = min(P.T - t0, W3_BM) * P.N * 4;  // bytes of the tile's valid rows, from its first row
-    const __amdgpu_buffer_rsrc_t ro_ = __builtin_amdgcn_make_buffer_rsrc(P.out + r0 * P.N, (short)0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr_ =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(P.res ? P.res + r0 * P.N : P.out), (short)0, nrec, 0x00020000);
-    const int cbase = (col0 + wn * 96 + (lane & 15)) * 4;
-    auto off = [&](int g, int rr, int j) {  // byte offset of (pair g = 2 i + h, row 2 h + rr, column j)
-      const int m = wm * 64 + (g >> 1) * 16 + (lane >> 4) * 4 + 2 * (g & 1) + rr;
-      return m * P.N * 4 + cbase + j * 64;
-    };
-    float rv[2][2][TN], pv[2][2][TN];
-    auto ld = [&](int g, float (&rvg)[2][TN], float (&pvg)[2][TN]) {
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          rvg[rr][j] = P.res ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_, off(g, rr, j), 0, 0))
-                             : 0.f;
-          pvg[rr][j] = P.accumulate
-                           ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ro_, off(g, rr, j), 0, 0))
-                           : 0.f;
-        }
-    };
-    ld(0, rv[0], pv[0]);
-#pragma unroll
-    for (int g = 0; g < 2 * TM; ++g) {
-      if (g + 1 < 2 * TM) ld(g + 1, rv[(g + 1) & 1], pv[(g + 1) & 1]);
-      const int i = g >> 1;
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const float v = (acc[i][j][2 * (g & 1) + rr] + bv[j] + rv[g & 1][rr][j]) * P.out_scale + pv[g & 1][rr][j];
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ro_, off(g, rr, j), 0, 0);
-        }
-    }
     }
   };
 
@@ -702,7 +658,6 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;
   if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
   if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
-  if ((int64_t)W3_BM * a.N * 4 >= (1ll << 31)) return 0;     // 32-bit buffer offsets of the fp32 epilogue
   P.nwg = (int)nt;
   const int ord = knobs().wconv_order;
   P.n_major = ord >= 0 ? ord : 1;
@@ -710,13 +665,8 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  if (knobs().xp[0] == 1) {  // (temporary A/B: the round-4 epilogue)
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, true>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, true>), dim3(grid), dim3(512), 0, s, P);
-  } else {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
-  }
+  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
     std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);
