@@ -629,285 +629,6 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// wconv5: wconv3's persistent (tile, chunk, tap) pipeline with FOUR waves, one per SIMD, each owning a 128 x 96 wave
-// tile (8 x 6 16x16x32 MFMAs per 32-deep slice): 14 fragment reads per 48 MFMAs instead of 10 per 24 (0.29 per MFMA,
-// 30 % fewer LDS bytes per flop), no SIMD partner contending for the matrix pipe.  The 192 accumulator registers live
-// in AGPRs (the MFMAs are inline asm with "+a" operands: the compiler's own allocation of this tile spilled 65
-// registers), the double-buffered fragments (112 VGPRs) in VGPRs.  Same LDS images, ring, counted waits and one
-// barrier per step as wconv3; each wave issues twice the DMA pieces (6 weight, 10 window per chunk).
-constexpr int W5_WPW = W3_WROWS / 8 / 4;  // window DMA instructions per wave (10)
-constexpr int W5_BPW = W3_BN / 8 / 4;     // weight DMA instructions per wave per step (6)
-
-template <int N>
-__device__ __forceinline__ void w5_wait_barrier() {
-  static_assert(N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
-  __builtin_amdgcn_s_barrier();
-}
-
-template <int PREC>
-__device__ __forceinline__ void w5_mfma(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  if constexpr (PREC == PREC_F16)
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-
-template <int PREC>
-__global__ __launch_bounds__(256, 1) void wconv5_kernel(const WConvDev P) {
-  constexpr int TM = 8, TN = 6;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
-  const int ntiles = P.nwg;
-  const int R = (ntiles + 7) >> 3;
-  const int tbeg = xcd * R, tend = min(tbeg + R, ntiles);
-  const int first = tbeg + slot;
-  const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
-  if (my_n == 0) return;
-  const int K = P.ksize, Cp = P.Cp, nC = Cp / 64;
-  const int WR = W3_BM + (K - 1) * P.dil;
-  const int total = my_n * nC * K;
-  const int nchunks = my_n * nC;
-  const int tiles_m = ntiles / P.tiles_n;
-  auto tile_of = [&](int ti, int& b, int& t0, int& col0) {
-    const int tile = first + ti * nslot;
-    int mt, nt;
-    if (P.n_major) {
-      nt = tile / tiles_m;
-      mt = tile - nt * tiles_m;
-    } else {
-      mt = tile / P.tiles_n;
-      nt = tile - mt * P.tiles_n;
-    }
-    b = mt / P.tiles_per_batch;
-    t0 = (mt - b * P.tiles_per_batch) * W3_BM;
-    col0 = nt * W3_BN;
-  };
-  const u16* wsrc_base = P.a;
-  int wrow0 = 0, wbuf = 0;
-  auto win_setup = [&](int q) {
-    const int ti = q / nC, c = q - ti * nC;
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
-    wsrc_base = P.a + (int64_t)b * P.T * Cp + c * 64;
-    wrow0 = t0 - P.pad;
-    wbuf = q & 1;
-  };
-  auto win_piece = [&](int j) {  // instruction j of the wave: rows 8 (wave + 4 j) .. + 7
-    const int row = 8 * (wave + 4 * j) + (lane >> 3);
-    const int ls = (lane & 7) ^ (row & 7);
-    const int ts = wrow0 + row;
-    const bool ok = row < WR && ts >= 0 && ts < P.T;
-    const u16* src = ok ? wsrc_base + (int64_t)ts * Cp + ls * 8 : reinterpret_cast<const u16*>(g_wconv_zero);
-    glds16(src, smem + wbuf * W3_WBUF + (wave + 4 * j) * 1024);
-  };
-  const int wspread = K - 2;
-  uint32_t boff[W5_BPW];
-#pragma unroll
-  for (int j = 0; j < W5_BPW; ++j) {
-    const int n = 8 * (wave + 4 * j) + (lane >> 3);
-    boff[j] = (uint32_t)(n * P.kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
-  }
-  int ig = 0, ic = 0, itap = 0, iti = 0;
-  int64_t iwoff;
-  {
-    int b_, t0_, col0_;
-    tile_of(0, b_, t0_, col0_);
-    iwoff = (int64_t)col0_ * P.kpad;
-  }
-  auto issue_wt = [&](int sl) {
-    const char* base = reinterpret_cast<const char*>(P.w + iwoff);
-#pragma unroll
-    for (int j = 0; j < W5_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 4 * j) * 1024);
-  };
-  auto advance_wt = [&]() {
-    if (++ig >= total) return;
-    iwoff += Cp;
-    if (++itap == K) {
-      itap = 0;
-      iwoff += 64 - (int64_t)K * Cp;
-      if (++ic == nC) {
-        ic = 0;
-        int b_, t0_, col0_;
-        tile_of(++iti, b_, t0_, col0_);
-        iwoff = (int64_t)col0_ * P.kpad;
-      }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int arow0 = wm * 128 + (lane & 15);
-  const int nrow0 = wn * 96 + (lane & 15);
-  const int bsw = lane & 7;
-  auto rdA = [&](int buf, int tp, int sub, int i) -> bf16x8 {
-    const int arow = arow0 + tp * P.dil;
-    return *reinterpret_cast<const bf16x8*>(smem + buf * W3_WBUF + arow * 128 +
-                                            (((4 * sub + (lane >> 4)) ^ (arow & 7)) << 4) + i * 16 * 128);
-  };
-  auto rdB = [&](int sl, int sub, int j) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(smem + 2 * W3_WBUF + sl * W3_BBUF + nrow0 * 128 +
-                                            (((4 * sub + (lane >> 4)) ^ bsw) << 4) + j * 16 * 128);
-  };
-
-  auto epilogue = [&](int ti) {
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
-    float bv[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
-    if (P.oplane) {
-      const bool odd = lane & 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-          const int r = 2 * rp + (odd ? 1 : 0);
-          const int t = t0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-          u16* const rowp = P.oplane + ((int64_t)b * P.T + min(t, P.T - 1)) * P.N + col0 + wn * 96 + (lane & 14);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const float v0 = acc[i][j][2 * rp] + bv[j] + 0.f, v1 = acc[i][j][2 * rp + 1] + bv[j] + 0.f;
-            const float send = odd ? v0 : v1;
-            const float recv = __builtin_bit_cast(
-                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, true));
-            const float lo = odd ? recv : v0, hi = odd ? v1 : recv;
-            if (t < P.T) op_store2<PREC>(rowp + j * 16, 0, f32x2{lo, hi});
-          }
-        }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      float rv[4][TN], pv[4][TN];
-      int orow[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = t0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-        orow[r] = t < P.T ? b * P.T + t : -1;
-        const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
-          pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (orow[r] < 0) continue;
-        const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
-      }
-    }
-  };
-
-  // prologue: window 0, weights 0, 1, 2
-  win_setup(0);
-#pragma unroll
-  for (int j = 0; j < W5_WPW; ++j) win_piece(j);
-  issue_wt(0);
-  advance_wt();
-  issue_wt(1);
-  advance_wt();
-  issue_wt(2);
-  advance_wt();
-  w5_wait_barrier<2 * W5_BPW>();
-  int pieces_last = 0;
-
-  bf16x8 aA[TM], aB[TM], bA[TN], bB[TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) aA[i] = rdA(0, 0, 0, i);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) bA[j] = rdB(0, 0, j);
-
-  int ti = 0, c = 0, tap = 0, sl = 0, q = 0;
-  auto mid_step = [&]() {
-    switch (pieces_last) {
-      case 0: w5_wait_barrier<W5_BPW>(); break;
-      case 1: w5_wait_barrier<W5_BPW + 1>(); break;
-      case 2: w5_wait_barrier<W5_BPW + 2>(); break;
-      case 3: w5_wait_barrier<W5_BPW + 3>(); break;
-      case 4: w5_wait_barrier<W5_BPW + 4>(); break;
-      case 5: w5_wait_barrier<W5_BPW + 5>(); break;
-      default: w5_wait_barrier<W5_BPW + W5_WPW>(); break;
-    }
-    pieces_last = 0;
-    if (tap < wspread && tap < W5_WPW && q + 1 < nchunks) {
-      if (tap == 0) win_setup(q + 1);
-      for (int j = tap; j < W5_WPW; j += wspread) {
-        win_piece(j);
-        ++pieces_last;
-      }
-    }
-  };
-  for (int g = 0; g < total; ++g) {
-    const bool chunk_end = tap == K - 1;
-    const int sl1 = sl == 2 ? 0 : sl + 1;
-    const int nbuf = chunk_end ? (q + 1) & 1 : q & 1;
-    const int ntap = chunk_end ? 0 : tap + 1;
-    // ---- slice 0 on (aA, bA); slice 1's fragments read after its first row
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) w5_mfma<PREC>(acc[i][j], aA[i], bA[j]);
-      if (i == 0) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bB[j] = rdB(sl, 1, j);
-#pragma unroll
-        for (int ii = 0; ii < TM; ++ii) aB[ii] = rdA(q & 1, tap, 1, ii);
-      }
-    }
-    mid_step();
-    // ---- slice 1 on (aB, bB); the next step's slice-0 fragments and weight step g + 3 issued after its first row
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) w5_mfma<PREC>(acc[i][j], aB[i], bB[j]);
-      if (i == 0) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bA[j] = rdB(sl1, 0, j);
-#pragma unroll
-        for (int ii = 0; ii < TM; ++ii) aA[ii] = rdA(nbuf, ntap, 0, ii);
-        issue_wt(sl);
-      }
-    }
-    advance_wt();
-    sl = sl1;
-    if (!chunk_end) {
-      ++tap;
-      continue;
-    }
-    tap = 0;
-    ++q;
-    if (++c == nC) {
-      // the last MFMAs' AGPR results before any VALU read (the hazard recognizer does not see inside inline asm)
-      asm volatile("s_nop 7");
-      asm volatile("s_nop 7");
-      asm volatile("s_nop 7");
-      asm volatile("s_nop 7");
-      epilogue(ti);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      asm volatile("s_nop 4");
-      c = 0;
-      ++ti;
-    }
-  }
-}
-
 static int g_ncu = 0;
 
 // Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
@@ -944,14 +665,8 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  const bool w5 = knobs().xp[1] == 1;  // (A/B: the 4-wave AGPR-accumulator build)
-  if (w5) {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv5_kernel<PREC_F16>), dim3(grid), dim3(256), 0, s, P);
-    else hipLaunchKernelGGL((wconv5_kernel<PREC_BF16>), dim3(grid), dim3(256), 0, s, P);
-  } else {
-    if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
-    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
-  }
+  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
     std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);

@@ -763,40 +763,3 @@ def test_conv1_fp16_handoff(K, C, T, k, dil, grid, monkeypatch):
         else:
             assert rel_l2(y16.cpu()[0].view(torch.float16).float().numpy(), y32.cpu().numpy()) < 1e-3
         assert torch.equal(act16, act32), f"activation on the fp16 plane differs, wconv3={w3}"
-
-
-@pytest.mark.parametrize("C,T,k,dil,grid,mode", [(768, 600, 11, 5, 8, "acc"), (384, 1100, 7, 3, 0, "res"),
-                                                 (192, 1500, 3, 1, 16, "acc"), (576, 467, 9, 1, 0, "res"),
-                                                 (192, 257, 11, 5, 0, "plane"), (384, 700, 3, 1, 8, "plane")])
-@pytest.mark.parametrize("prec", [0, 2])
-def test_wconv5_matches_wconv3(K, C, T, k, dil, grid, mode, prec, monkeypatch):
-    """The 4-wave wide conv with AGPR accumulators (wconv5, ALCM_XP1=1 while it is A/B-tested) issues every
-    accumulator's MFMAs in wconv3's (chunk, tap, slice) order: bit-identical outputs on the fp32 epilogue (residual,
-    accumulate, masked rows of a partial last tile) and the fp16 plane epilogue, several tiles per workgroup."""
-    from audiolcm_amd import _hip
-    B = 2
-    x = _r((B, T, C), 170)
-    w, bias = _r((C, C, k), 171, 0.7 / np.sqrt(C * k)), _r((C,), 172, 0.05)
-    r = dev(_r((B, T, C), 173))
-    pl = K.operand_planes(dev(x), prec)
-    outs = []
-    for xp in ("0", "1"):
-        for kk, v in (("ALCM_WCONV3", "1"), ("ALCM_WCONV3_GRID", str(grid)), ("ALCM_XP1", xp)):
-            monkeypatch.setenv(kk, v)
-        _hip.reload_knobs()
-        try:
-            if mode == "plane":
-                outs.append(K.opconv(pl, C, dev(w), dev(bias), dil, prec, out_plane=True).cpu())
-            else:
-                o = dev(_r((B, T, C), 174)) if mode == "acc" else None
-                outs.append(K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=r, out_scale=0.5,
-                                     accumulate_into=o).cpu())
-        finally:
-            for kk in ("ALCM_WCONV3", "ALCM_WCONV3_GRID", "ALCM_XP1"):
-                monkeypatch.delenv(kk)
-            _hip.reload_knobs()
-    assert torch.equal(outs[0], outs[1])
-    if mode != "plane":
-        ref = F.conv1d(x.permute(0, 2, 1), w, bias, dilation=dil, padding=(k - 1) * dil // 2).permute(0, 2, 1)
-        ref = (ref + r.cpu()) * 0.5 + (_r((B, T, C), 174) if mode == "acc" else 0)
-        assert rel_l2(outs[1].numpy(), ref.numpy()) < TOL[prec]
