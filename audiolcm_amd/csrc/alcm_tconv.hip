@@ -502,9 +502,7 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   // streamed weights (two workgroups per CU) where the resident weights would take a CU's LDS: C >= 48
   const int tk = knobs().tconv;
   // measured per launch (scripts/microbench.py tconv): streamed wins at C = 96 and C = 24, resident at C = 48
-  const int xpw = knobs().xp[2];  // (experiment: streamed persistent grids of xpw workgroups per CU for every width, so
-                                  // the three resblock chains' launches can share CUs)
-  const bool streamed = xpw > 0 || tk == 2 || (tk != 3 && C != 48);
+  const bool streamed = tk == 2 || (tk != 3 && C != 48);
   const bool small = streamed && C != 96 && knobs().tconv_bm == 128;  // 128-row tiles, three workgroups per CU
   const int BM = small ? 128 : (C == 96 ? 192 : 256);
   const int NS = (!streamed && C == 96) ? 48 : C;
@@ -523,12 +521,7 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     // one workgroup per tile (persistent measured +5..+17 %)
     int grid2 = (int)nt;
     const int stg = knobs().tconv_stagger >= 0 ? knobs().tconv_stagger : (C == 96 ? 3 : 0);
-    if (xpw > 0) {
-      int dev = 0, ncu = 256;
-      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * xpw);
-      P.stagger = 0;
-    } else if (stg > 0) {
+    if (stg > 0) {
       int dev = 0, ncu = 256;
       if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * (small ? 3 : 2));
