@@ -228,9 +228,9 @@ template <int TT>
 struct AmGeo {
   static constexpr int XR = TT + 16;                   // staged x rows
   static constexpr int UPB = (2 * TT + 10 + 15) / 16;  // up blocks
-  static constexpr int SS = UPB * 16 + 4;              // sample stride in pairs (/4 odd)
-  static constexpr int OCC = TT == 48 ? 3 : 2;
-  static_assert(XR <= AM_XS && (SS / 4) % 2 == 1 && 8 * (UPB - 1) + 15 < XR && TT % 16 == 0, "act_mfma tile");
+  static constexpr int OCC = 4;                        // workgroups per CU (31 KB of LDS, <= 128 VGPRs)
+  static_assert(XR <= AM_XS && 8 * (UPB - 1) + 15 < XR && TT % 16 == 0 && 2 * (TT / 16 - 1) + 2 < UPB,
+                "act_mfma tile");
 };
 
 // IN16: x is an fp16 plane [B][T][C] (a conv1 that wrote its output in the format this kernel rounds its input to:
@@ -242,12 +242,11 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
                                                                           const float* __restrict__ ibeta,
                                                                           const Taps12O f, int strips_t, int tiles_c) {
   constexpr float INV_PI = 0.318309886183790671538f;
-  constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_SS = AmGeo<TT>::SS, AM_UPB = AmGeo<TT>::UPB;
+  constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_UPB = AmGeo<TT>::UPB;
   // per wave [16 ch][XS rows] of (v, v) pairs; waves 4 pairs apart (= 4 mod 64 banks: the cooperative writes below
   // are conflict-free)
   constexpr int XWS = 16 * AM_XS + 4;
   __shared__ __attribute__((aligned(16))) uint32_t xs[4 * XWS];
-  __shared__ __attribute__((aligned(16))) uint32_t ss[4][16 * AM_SS];
   // the workgroup's output tile [TT rows][64 channels] (row stride 72 halves), written out as whole 128-B row segments
   // (each wave's own 32-B pieces of 16 rows left partial lines for the L2 to merge: 1.7x the plane bytes in PMC)
   constexpr int OS = 72;
@@ -262,7 +261,6 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
   const int c0 = ct * 64 + wave * 16;
   const int tile0 = st * AM_STRIP, ntile = min(AM_STRIP, (T + AM_TT - 1) / AM_TT - tile0);
   uint32_t* const xw = xs + wave * XWS;
-  uint32_t* const sw = ss[wave];
 
   // tap fragments, once per strip: up A[q = l16][k = 8 q4 + e] = tap_(e&1)[ku], ku = q - 2 r' + 10, r' = 4 q4 + e / 2
   // (x row of the block); down B[k][n = l16] = tap_(e&1)[i' - 2 n], i' = 16 p + 4 q4 + e / 2 (sample of the block)
@@ -284,12 +282,6 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
       const _Float16 hi = (_Float16)tv;
       bdn[p][e] = (e & 1) ? (_Float16)(tv - (float)hi) : hi;
     }
-  // samples AM_UPB * 16 .. AM_SS - 1 of each channel row are read by the last down blocks against zero taps but never
-  // written: zero them once (uninitialised LDS could hold NaN bit patterns, and NaN * 0 = NaN)
-  if (q4 == 0) {
-#pragma unroll
-    for (int i = AM_UPB * 16; i < AM_SS; ++i) sw[l16 * AM_SS + i] = 0u;
-  }
   const int cl = c0 + l16;  // this lane's channel in the up products
   const float ear = aexp[cl] * INV_PI, hh = ibeta[cl] * 0.5f;
 
@@ -352,49 +344,59 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
     // every wave's x pairs staged: LDS-only wait (a __syncthreads fence would also wait for the prefetch)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
-    // up blocks: samples i = 16 bk + 4 q4 + r of channel l16 -> SnakeBeta (fp32) -> (s, s) pairs at sw[l16 SS + i]
+    // up blocks: samples i = 16 bk + 4 q4 + r of channel l16 -> SnakeBeta (fp32) -> (s, s) pairs, kept in registers: the
+    // MFMA output fragment of up block bk (lane (q4, l16): channel l16, samples 16 bk + 4 q4 .. + 3) is exactly the A
+    // fragment of the down block reading samples 16 bk .. + 15 (row = channel l16, k-group q4), so the samples never
+    // go through LDS (round 4 staged them: 84 KB of the tile's 156 KB of LDS traffic)
+    uint4 sf[AM_UPB];
 #pragma unroll
     for (int bk = 0; bk < AM_UPB; ++bk) {
       const f16x8 bx = *reinterpret_cast<const f16x8*>(xw + l16 * AM_XS + 8 * bk + 4 * q4);
       const f32x4 u = __builtin_amdgcn_mfma_f32_16x16x32_f16(aup, bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      uint4 o;
-      uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+      uint32_t* op = reinterpret_cast<uint32_t*>(&sf[bk]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float sv = fmaf(-hh, __builtin_amdgcn_cosf(u[r] * ear), u[r] + hh);
         op[r] = am_pair(sv);
       }
-      *reinterpret_cast<uint4*>(sw + l16 * AM_SS + 16 * bk + 4 * q4) = o;
     }
-    // DownSample1d replicate padding: samples m = 2 t0 - 5 + i outside [0, 2T) take s(0) / s(2T - 1)
+    // DownSample1d replicate padding: samples m = 2 t0 - 5 + i outside [0, 2T) take s(0) / s(2T - 1) (wave-uniform:
+    // only the tiles at a clip's ends): the pair at local index i_lo / i_hi of this lane's channel, from the lane
+    // holding it (q4 = (i >> 2) & 3, same l16)
     const int i_lo = 5 - 2 * t0, i_hi = 2 * T + 4 - 2 * t0;  // local indices of m = 0 and m = 2T - 1
     if (i_lo > 0 || i_hi < AM_UPB * 16 - 1) {
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-      if (q4 == 0) {
-        uint32_t* row = sw + l16 * AM_SS;
-        if (i_lo > 0) {
-          const uint32_t v0 = row[i_lo];
-          for (int i = 0; i < i_lo; ++i) row[i] = v0;
+      auto pick = [&](int i) -> uint32_t {  // this lane's pair r = i & 3 of block i >> 4 (selects: register arrays)
+        uint32_t v = 0u;
+#pragma unroll
+        for (int bk = 0; bk < AM_UPB; ++bk) {
+          const uint32_t* sp = reinterpret_cast<const uint32_t*>(&sf[bk]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v = (bk == (i >> 4) && r == (i & 3)) ? sp[r] : v;
         }
-        if (i_hi >= 0 && i_hi < AM_UPB * 16 - 1) {
-          const uint32_t v1 = row[i_hi];
-          for (int i = i_hi + 1; i < AM_UPB * 16; ++i) row[i] = v1;
+        return v;
+      };
+      const int il = max(i_lo, 0), ih = min(max(i_hi, 0), AM_UPB * 16 - 1);
+      const uint32_t vlo = (uint32_t)__shfl((int)pick(il), ((il >> 2) & 3) * 16 + l16);
+      const uint32_t vhi = (uint32_t)__shfl((int)pick(ih), ((ih >> 2) & 3) * 16 + l16);
+#pragma unroll
+      for (int bk = 0; bk < AM_UPB; ++bk) {
+        uint32_t* sp = reinterpret_cast<uint32_t*>(&sf[bk]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * bk + 4 * q4 + r;
+          if (i_lo > 0 && i < i_lo) sp[r] = vlo;
+          if (i_hi >= 0 && i_hi < AM_UPB * 16 - 1 && i > i_hi) sp[r] = vhi;
         }
       }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
 
     // down blocks: outputs j = t0 + 16 d + l16, channels c0 + 4 q4 .. + 3 -> 8-B fp16 plane stores
 #pragma unroll
     for (int d = 0; d < AM_TT / 16; ++d) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const f16x8 a = *reinterpret_cast<const f16x8*>(sw + l16 * AM_SS + 32 * d + 16 * p + 4 * q4);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bdn[p], acc, 0, 0, 0);
-      }
+      for (int p = 0; p < 3; ++p)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, sf[2 * d + p]), bdn[p], acc, 0, 0, 0);
       uint2 w;
       w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
       w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
