@@ -289,20 +289,17 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
   // w's instruction it covers rows 16 it + 4 w .. + 3, lane = (row, 16-B piece); each piece belongs to the wave
   // owning its 16 channels.  The next tile's rows are loaded into registers while this tile computes
   // (each wave loading its own 16 channels as 64-B row pieces measured 8.32 vs 8.18 ms/step, profiles/r4ae)
-  // (IN16: 16-B pieces of eight fp16 channels, 8 lanes per 128-B row segment: wave w's instruction it covers rows
-  // 32 it + 8 w .. + 7, rows >= XR not loaded; 8-B pieces at the fp32 kernel's lane mapping read 25 % slower)
-  typedef typename std::conditional<IN16, uint4, float4>::type XPiece;
-  constexpr int NXI = IN16 ? (AM_XR + 31) / 32 : AM_XR / 16;  // x load instructions per lane
+  // (IN16: the same lanes and rows, 8-B pieces of four fp16 channels: 128-B row segments)
+  typedef typename std::conditional<IN16, uint2, float4>::type XPiece;
   const char* const xb = reinterpret_cast<const char*>(xin) +
-                         (IN16 ? ((int64_t)b * T * C + ct * 64 + (lane & 7) * 8) * 2
-                               : ((int64_t)b * T * C + ct * 64 + (lane & 15) * 4) * 4);
-  XPiece xv[NXI];
-  auto xrow = [&](int it) { return IN16 ? it * 32 + wave * 8 + (lane >> 3) : it * 16 + wave * 4 + (lane >> 4); };
+                         ((int64_t)b * T * C + ct * 64 + (lane & 15) * 4) * (IN16 ? 2 : 4);
+  XPiece xv[AM_XR / 16];
+  auto xrow = [&](int it) { return it * 16 + wave * 4 + (lane >> 4); };
   auto load_x = [&](int t0) {
 #pragma unroll
-    for (int it = 0; it < NXI; ++it) {
+    for (int it = 0; it < AM_XR / 16; ++it) {
       const int t = min(max(t0 - 5 + xrow(it), 0), T - 1);
-      if (!IN16 || xrow(it) < AM_XR) xv[it] = *reinterpret_cast<const XPiece*>(xb + (int64_t)t * C * (IN16 ? 2 : 4));
+      xv[it] = *reinterpret_cast<const XPiece*>(xb + (int64_t)t * C * (IN16 ? 2 : 4));
     }
   };
   load_x(tile0 * AM_TT);
@@ -322,27 +319,19 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
   for (int tl = 0; tl < ntile; ++tl) {
     const int t0 = (tile0 + tl) * AM_TT;
     // (v, v) fp16 pairs at xw'[c * XS + r] of the owning wave w'
-    if constexpr (IN16) {  // lane's 8 channels 8 (lane & 7) .. + 7: owning wave (lane & 7) >> 1, c = 8 (lane & 1)
-      uint32_t* const xo = xs + ((lane & 7) >> 1) * XWS;
-      const int c = (lane & 1) * 8;
-#pragma unroll
-      for (int it = 0; it < NXI; ++it) {
-        const int r = xrow(it);
-        if (r >= AM_XR) continue;
-        const uint32_t hw[4] = {xv[it].x, xv[it].y, xv[it].z, xv[it].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          xo[(c + 2 * k) * AM_XS + r] = (hw[k] & 0xffffu) | (hw[k] << 16);
-          xo[(c + 2 * k + 1) * AM_XS + r] = (hw[k] >> 16) | (hw[k] & 0xffff0000u);
-        }
-      }
-    } else {
+    {
       uint32_t* const xo = xs + ((lane & 15) >> 2) * XWS;
       const int c = (lane & 3) * 4;
 #pragma unroll
-      for (int it = 0; it < NXI; ++it) {
+      for (int it = 0; it < AM_XR / 16; ++it) {
         const int r = xrow(it);
-        {
+        if constexpr (IN16) {
+          const uint2 h = xv[it];
+          xo[(c + 0) * AM_XS + r] = (h.x & 0xffffu) | (h.x << 16);
+          xo[(c + 1) * AM_XS + r] = (h.x >> 16) | (h.x & 0xffff0000u);
+          xo[(c + 2) * AM_XS + r] = (h.y & 0xffffu) | (h.y << 16);
+          xo[(c + 3) * AM_XS + r] = (h.y >> 16) | (h.y & 0xffff0000u);
+        } else {
           xo[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
           xo[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
           xo[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
