@@ -80,21 +80,6 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
         if (n < NS) ot[m * OTS + n] = acc[i][j][r] + bias_r[j];
       }
     }
-  // residual rows not prefetched before the K loop (C = 96: 18 float4 per thread): every load issued here in one burst
-  // into the registers the accumulators just vacated, so the loop below waits for them once (loaded one per iteration,
-  // next to the state stores, each waited for its own round trip: the launch's waves were parked 66 % of their cycles,
-  // scripts/pmc_tconv.sh)
-  constexpr bool LATE = RES && !PRE;
-  float4 rl[LATE ? NRES : 1];
-  const bool burst = LATE && !(P.ablate & 8);  // (ALCM_TCONV_ABLATE=8: one load per iteration, the A/B reference)
-  if (burst) {
-#pragma unroll
-    for (int i = 0; i < NRES; ++i) {
-      const int e = min(tid + i * NT, BM * (NS / 4) - 1);
-      const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
-      rl[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + min(max(t0 + m, 0), P.T - 1)) * P.N + n0 + n);
-    }
-  }
   __syncthreads();
   const int e_hi = min(e0 + E, P.T);
   if constexpr (RES || OUTW || ACC) {
@@ -109,7 +94,6 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
       if constexpr (RES) {
         float4 r4;
         if constexpr (PRE) r4 = rv[PRE ? i : 0];
-        else if (burst) r4 = rl[LATE ? i : 0];
         else r4 = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + min(max(t, 0), P.T - 1)) * P.N + n0 + n);
         v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
         if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
