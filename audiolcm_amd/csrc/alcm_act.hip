@@ -159,8 +159,7 @@ int act_coop(const float* x, void* const* y, int nset, int B, int T, int C, int 
   if (nset != 1 && nset != 3) return set_error(ALCM_E_INVALID, "activation1d: 1 or 3 parameter sets");
   // 64-channel tiles (whole 128-B output lines) measured faster at C = 768 (-15 %) and for the two-plane split
   // output (-10 %), slower at C = 384 (+10..15 %), even at C = 192 fp16 (scripts/microbench.py actnp)
-  const int knp = knobs().act_np;
-  const bool wide = Cp % 64 == 0 && (knp == 32 || (knp == 0 && (C >= 768 || prec == PREC_SPLIT)));
+  const bool wide = Cp % 64 == 0 && (C >= 768 || prec == PREC_SPLIT);
   const int np = wide ? 32 : 16, tt = 2048 / np;
   const int tiles_t = (T + tt - 1) / tt, tiles_c = Cp / (2 * np);
   const int64_t nwg = (int64_t)B * tiles_t * tiles_c;

@@ -429,7 +429,7 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
     const int Lp = (L + FA_KT - 1) / FA_KT * FA_KT;
     const int dh = nh > 0 ? H / nh : 0;
     if (qkv || (!O && !o_plane) || B <= 0 || L <= 0 || nh <= 0 || H % nh || dh > FR_MAXDH || dh % 4 || Lp > FR_MAXL ||
-        (prec != PREC_F16 && prec != PREC_BF16) || (((uintptr_t)qkv_plane) & 7) || knobs().attn_tiled ||
+        (prec != PREC_F16 && prec != PREC_BF16) || (((uintptr_t)qkv_plane) & 7) ||
         (bias && bld < L))
       return set_error(ALCM_E_INVALID, "flash_attention: bad plane-input arguments");
     const float scale = scale_in > 0.f ? scale_in : 1.0f / std::sqrt((float)dh);
@@ -456,7 +456,7 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
   const float scale = scale_in > 0.f ? scale_in : 1.0f / std::sqrt((float)dh);
   if (bias && bld < L) return set_error(ALCM_E_INVALID, "flash_attention: bias pitch < L");
   const int Lp = (L + FA_KT - 1) / FA_KT * FA_KT;
-  if (Lp <= FR_MAXL && dh <= FR_MAXDH && !knobs().attn_tiled && (int64_t)B * nh < (1ll << 31)) {
+  if (Lp <= FR_MAXL && dh <= FR_MAXDH && (int64_t)B * nh < (1ll << 31)) {
     void* tok = prof_start(s);
     const dim3 grid((unsigned)(B * nh));
     auto kern = prec == PREC_F16

@@ -105,44 +105,18 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
 // diagnostic / A-B switches, read from ALCM_* environment variables at library load (alcm_knobs.cpp)
 struct Knobs {
   int wconv = 8;                 // ALCM_WCONV: > 0 = the wide-layer kernels (alcm_wconv.hip), 0 = opconv_kernel (A/B)
-  int wconv_order = -1;          // ALCM_WCONV_ORDER: wconv2 workgroup order (-1 by shape, 0 M-tile major, 1 N-tile major)
   int wconv3 = -1;               // ALCM_WCONV3: persistent 8-wave 256 x 192 wide conv (alcm_wconv.hip): -1 by shape, 0 off, 1 on
   int wconv3_grid = 0;           // ALCM_WCONV3_GRID: cap on wconv3's persistent workgroups (tests; 0 = one per CU)
-  int wconv_tile = -1;           // ALCM_WCONV_TILE: wconv2 tile, 0 = 128 x 192, 1 = 256 x 96, -1 = by shape
   int nconv = -1;                // ALCM_NCONV: 0 = opconv_kernel for the narrow tail, 2 = nconv for every width
-  int nconv_nb = 0;              // ALCM_NCONV_NB: narrow-conv ring depth / tile variant
-  int act_rows = 8;              // ALCM_ACT_ROWS: rows per thread of the per-thread Activation1d kernel
-  bool act_v1 = false;           // ALCM_ACT_V1: per-thread Activation1d kernel instead of the cooperative one
-  bool ups_fp32 = false;         // ALCM_UPS_FP32: BigVGAN upsamplers on the fp32-operand conv at the base precision
-  int act_np = 0;                // ALCM_ACT_NP: channel pairs per cooperative Activation1d tile (0 by shape, 16, 32)
   int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
-  bool no_act_fusion = false;    // ALCM_NO_ACT_FUSION
-  bool no_flash = false;         // ALCM_NO_FLASH
-  bool attn_tiled = false;       // ALCM_ATTN_TILED: 64-query tiled flash kernel even where K/V fit in LDS
-  bool no_attn_planes = false;   // ALCM_NO_ATTN_PLANES
-  bool no_ffn_planes = false;    // ALCM_NO_FFN_PLANES
-  bool no_vae_planes = false;    // ALCM_NO_VAE_PLANES
-  bool tail_f16w2_all = false;   // ALCM_TAIL_F16W2_ALL
   bool serial_resblocks = false; // ALCM_SERIAL_RESBLOCKS: default of alcm_model_set_resblock_streams
   bool prof_shapes = false;      // ALCM_PROF_SHAPES: split profile rows per layer shape
-  int opconv_ablate = 0;         // ALCM_OPCONV_ABLATE: timing-only ablation bits of opconv_kernel (1 no epilogue,
-                                 // 2 no MFMA)
   int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
                                  // 2 no MFMA, 4 no window DMA)
-  int qkv_plane = 1;             // ALCM_QKV_PLANE: DiT q/k/v projection writes an fp16 plane for the attention (0 = fp32)
-  int text_flash = 1;            // ALCM_TEXT_FLASH: text-encoder attention in the fused kernel (0 = GEMM + softmax + GEMM)
-  int act3 = 1;                  // ALCM_ACT3: a tail stage's three first Activation1d in one pass (0 = one per chain)
-  int ups2 = 1;                  // ALCM_UPS2: stage 4-5 upsamplers as one two-phase split kernel (alcm_ups.hip), 0 = per-phase GEMMs
   int lin1 = -1;                 // ALCM_LIN1: single-plane 1x1 convs on lin_plane_kernel (1: 32-deep 4-stage ring, 2: 64-deep
                                  // double-buffered, -1: 64-deep for plane outputs), 0 = wconv2
-  int sgemm = 1;                 // ALCM_SGEMM: bf16x3 1x1 convs on split planes (alcm_sgemm.hip), 0 = gemm_kernel
-  int tconv_bm = 256;            // ALCM_TCONV_BM: 128 = 128-row tiles for the streamed narrow conv (C = 48 / 24)
-  bool post_planes = false;      // ALCM_POST_PLANES: BigVGAN output head as Activation1d planes + split conv (not fused)
-  int tconv_stagger = -1;        // ALCM_TCONV_STAGGER: streamed narrow conv grid: -1 by shape, 0 one workgroup per tile, >= 1 persistent (stagger - 1 sleeps)
-  int tconv_wgs = 0;             // ALCM_TCONV_WGS: persistent workgroups per CU of tconv_kernel's grid (0 by shape)
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,
                                  // 3 resident weights (alcm_tconv.hip), 0 = opconv / nconv
-  int tail_prefetch = 1;         // ALCM_TAIL_PREFETCH: narrow fused-activation convs prefetch the residual
   int act_defer = 1;             // ALCM_ACT_DEFER: act_mfma issues a tile's plane stores one tile late, before the next
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)

@@ -724,7 +724,7 @@ static DitWs plan_dit(const DitW& D, Bump& bp, int B, int T) {
 static int dit_attention(hipStream_t s, int split, const DitW& D, int B, int L, const float* qkv, float* S, float* O) {
   const int H = D.hidden, nh = D.heads, dh = H / nh, Lp = round_up(L, 8);
   // single-rounding policies: fused kernel, scores never leave the chip (alcm_attn.hip)
-  if ((split == PREC_F16 || split == PREC_BF16) && dh <= 72 && dh % 4 == 0 && !knobs().no_flash)
+  if ((split == PREC_F16 || split == PREC_BF16) && dh <= 72 && dh % 4 == 0)
     return flash_attention(qkv, O, B, L, H, nh, split, s);
   alcm_gemm_args g;
   std::memset(&g, 0, sizeof(g));
@@ -846,8 +846,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       ALCM_TRY(conv(s, split, B, L, hv, blk.proj_in, uo, o));
     }
     // BasicTransformerBlock (concatDiT.py:120-125)
-    const bool planes = (pff == PREC_F16 || pff == PREC_BF16) && (H / D.heads) <= 72 && (H / D.heads) % 4 == 0 &&
-                        !knobs().no_attn_planes;
+    const bool planes = (pff == PREC_F16 || pff == PREC_BF16) && (H / D.heads) <= 72 && (H / D.heads) % 4 == 0;
     for (int a = 0; a < 2 && planes; ++a) {
       // attention sub-block on operand planes: LayerNorm -> plane, fused q/k/v projection (k = 1 on the
       // wide-layer kernel), flash attention writing the to_out operand plane, to_out + bias + residual in place
@@ -863,7 +862,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       g.w = wq.w.p; g.w_lo_off = wq.w.lo; g.kpad = wq.w.kpad; g.N = wq.w.rows;
       g.bias = wq.b; g.out = w.qkv; g.out_scale = 1.f; g.prec = pff;
       // q / k / v as an operand plane (attention rounds them to pff anyway): half the bytes written and staged
-      const bool qp = knobs().qkv_plane && wq.w.rows % 4 == 0 && L <= 512 && !knobs().attn_tiled;
+      const bool qp = wq.w.rows % 4 == 0 && L <= 512;
       if (qp) {
         g.out = nullptr;
         g.out_plane = w.qkv;
@@ -888,7 +887,7 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       oo.res = ur;
       ALCM_TRY(conv(s, pff, B, L, ov, a ? blk.out2 : blk.out1, uo, oo));
     }
-    if ((pff == PREC_F16 || pff == PREC_BF16) && !knobs().no_ffn_planes) {
+    if (pff == PREC_F16 || pff == PREC_BF16) {
       // Conv1dFeedForward on operand planes and the wide-layer kernel (alcm_wconv.hip): LayerNorm -> plane,
       // conv k9 576 -> 2x2304 with the GEGLU epilogue writing the 2304-channel plane, conv k9 2304 -> 576
       // + bias + residual in place (non-overlapping tiles)
@@ -946,9 +945,9 @@ struct VaeWs {
   float *a, *b, *c, *d, *qkv, *S, *gsc, *gsh, *pqs, *pqh;
   u16* pl;  // operand plane of the k3 conv inputs (F16 / BF16 layers)
 };
-// the VAE's k3 convs read operand planes on the wide-layer kernel unless ALCM_NO_VAE_PLANES is set
+// the VAE's k3 convs read operand planes on the wide-layer kernel
 static bool vae_planes(int pk3) {
-  return (pk3 == PREC_F16 || pk3 == PREC_BF16) && !knobs().no_vae_planes;
+  return pk3 == PREC_F16 || pk3 == PREC_BF16;
 }
 // conv k3 (same length) on an operand plane: out = conv(plane) + bias (+ res); out may alias res
 static int plane_conv3(hipStream_t s, int prec, int B, int T, int C, const u16* plane, const ConvW& cw,
@@ -1309,8 +1308,7 @@ static int voc_prec(const alcm_model* m, int si) {
   if (m->policy == ALCM_POLICY_SPLIT) return PREC_SPLIT;
   // stage 3 (C = 96, the costliest tail stage) tolerates fp16 weights: +1e-5 waveform rel-L2 emulated,
   // vs +2.5e-4 (stage 4) and +4.3e-4 (stage 5) (scripts/precision_emulate.py 96 tail)
-  const int f16_upto = knobs().tail_f16w2_all ? 3 : 4;  // diagnostics / A-B
-  return si < f16_upto ? PREC_F16 : PREC_F16W2;
+  return si < 4 ? PREC_F16 : PREC_F16W2;
 }
 
 static int act_planes(hipStream_t s, const ActW& a, const float* x, const VocWs& w, int B, int T, int C, int prec,
@@ -1436,7 +1434,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const bool wide_ok = S.cout % 192 == 0 && S.cin % 64 == 0 && S.phase[0].w.taps - 1 <= 64;
     const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cin % 32 == 0 &&
                             (wide_ok || (S.cout <= 96 && S.cout % 4 == 0)) &&
-                            S.phase[0].w.cpad == S.cin && !knobs().ups_fp32;
+                            S.phase[0].w.cpad == S.cin;
     if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
     // the split-precision stride-2 stages with the kernel's widths (stages 4-5): both phases in one pass over x
     const bool ups_two = !ups_planes && split == PREC_SPLIT && S.rate == 2 &&
@@ -1476,8 +1474,8 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const bool conc = ax != nullptr;
     // the wide stages' conv1 -> Activation1d hand-off as an fp16 plane (ALCM_CONV1_H16=0: fp32, the A/B reference)
     const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
-    // the three chains' first Activation1d in one pass over u (their own planes, same taps; ALCM_ACT3=0: one per chain)
-    bool act3 = conc && fuse && S.rb.size() == 3 && knobs().act3 &&
+    // the three chains' first Activation1d in one pass over u (their own planes, same taps)
+    bool act3 = conc && fuse && S.rb.size() == 3 &&
                 !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
     for (size_t j = 1; act3 && j < S.rb.size(); ++j)
       act3 = !std::memcmp(S.rb[j].act[0].fup, S.rb[0].act[0].fup, sizeof(S.rb[0].act[0].fup)) &&
@@ -1544,7 +1542,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   // conv_post maps 24 channels to the waveform: its input rounding shows up 1:1 in the output, so the
   // mixed policy keeps it bf16x3 (one launch, ~5e-4 of the waveform error budget otherwise)
   const int ppost = m->policy == ALCM_POLICY_BF16 ? PREC_BF16 : PREC_SPLIT;
-  if (ppost == PREC_SPLIT && G.st.back().cout == 24 && G.post_w32 && !knobs().post_planes) {
+  if (ppost == PREC_SPLIT && G.st.back().cout == 24 && G.post_w32) {
     // one fused fp32 launch (alcm_act.hip post_kernel): exact fp32 where the split path approximates it
     Taps12O f;
     for (int k = 0; k < 12; ++k) {
@@ -1767,8 +1765,8 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
   // an in-kernel conversion ran the text towers at 0.05 of the MFMA peak (profiles/r3z, bench components)
   const bool planes = (pl == PREC_F16 || pl == PREC_BF16) && H % 64 == 0 && D % 64 == 0 && TI % 64 == 0 &&
                       X.b_inter % 64 == 0 && X.t_ff % 64 == 0;
-  // attention of both towers in the fused kernel (ALCM_TEXT_FLASH=0: score GEMM + softmax + PV GEMM)
-  const bool tflash = planes && knobs().text_flash && !knobs().attn_tiled && L <= 512 && H / X.b_heads <= 72 && X.t_dkv <= 72 &&
+  // attention of both towers in the fused kernel
+  const bool tflash = planes && L <= 512 && H / X.b_heads <= 72 && X.t_dkv <= 72 &&
                       (H / X.b_heads) % 4 == 0 && X.t_dkv % 4 == 0;
   for (const BertLayerW& Ly : X.bl) {
     if (planes) {

@@ -276,18 +276,14 @@ int nconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
   P.w = wplane; P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   if (act) P.act = *reinterpret_cast<const ActEpiDev*>(actepi);
-  P.act_prefetch = knobs().tail_prefetch;
+  P.act_prefetch = 1;
   // tile configurations (rows per tile, weight ring depth) sized for >= 2 workgroups per CU where the LDS
   // allows: C = 24 -> 256 x 32, 4 buffers (36 KB, 4 workgroups per CU); C = 48 -> 256 x 64, 4 buffers (72 KB);
   // C = 96 -> 128 x 96, 3 buffers (72 KB)
   int BM, BN, NB;
-  // diagnostics / A-B (ALCM_NCONV_NB set): C = 24 ring depth 8 instead of 4 when it is "8"; C = 48 / 96 take
-  // 128-row tiles with 3 / 2 ring buffers (3 workgroups per CU) — measured equal to opconv_kernel there
-  const bool nbe = knobs().nconv_nb != 0;
-  const int nb32 = knobs().nconv_nb == 8 ? 8 : 4;  // 4: 36 KB LDS -> 4 workgroups/CU (measured -12%)
-  if (a.N <= 32 && a.Cp == 32) BM = 256, BN = 32, NB = nb32;
-  else if (a.N <= 64 && a.Cp == 64) BM = nbe ? 128 : 256, BN = 64, NB = nbe ? 3 : 4;
-  else if (a.N <= 96 && a.Cp == 96) BM = 128, BN = 96, NB = nbe ? 2 : 3;
+  if (a.N <= 32 && a.Cp == 32) BM = 256, BN = 32, NB = 4;
+  else if (a.N <= 64 && a.Cp == 64) BM = 256, BN = 64, NB = 4;
+  else if (a.N <= 96 && a.Cp == 96) BM = 128, BN = 96, NB = 3;
   else return 0;
   P.tstride = act ? BM - 2 * ACT_EPI_HALO : BM;
   P.tshift = act ? ACT_EPI_HALO : 0;
@@ -311,15 +307,9 @@ int nconv_try(const alcm_opconv_args& a, const u16* wplane, const void* actepi, 
     }
   };
   using std::integral_constant;
-  if (BN == 32 && NB == 4)
+  if (BN == 32)
     go(integral_constant<int, 256>{}, integral_constant<int, 32>{}, integral_constant<int, 1>{}, integral_constant<int, 4>{});
-  else if (BN == 32)
-    go(integral_constant<int, 256>{}, integral_constant<int, 32>{}, integral_constant<int, 1>{}, integral_constant<int, 8>{});
-  else if (BN == 64 && BM == 128)
-    go(integral_constant<int, 128>{}, integral_constant<int, 64>{}, integral_constant<int, 2>{}, integral_constant<int, 3>{});
   else if (BN == 64) go(integral_constant<int, 256>{}, integral_constant<int, 64>{}, integral_constant<int, 2>{}, integral_constant<int, 4>{});
-  else if (NB == 2)
-    go(integral_constant<int, 128>{}, integral_constant<int, 96>{}, integral_constant<int, 3>{}, integral_constant<int, 2>{});
   else go(integral_constant<int, 128>{}, integral_constant<int, 96>{}, integral_constant<int, 3>{}, integral_constant<int, 3>{});
   if (tok) {
     char name[112];  // the demangled rocprofv3 name of the instantiation

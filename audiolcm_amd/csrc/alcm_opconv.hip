@@ -2,9 +2,10 @@
 //
 // An AMPBlock1 half-layer (vocoder/bigvgan/models.py:72-81) is  y = conv_{k,d}(Activation1d(x)) + b.
 // Here it runs as two kernels:
-//   act_op_kernel   Activation1d (alias_free_torch/act.py:23-27: up-FIR x2 -> SnakeBeta -> down-FIR)
+//   activation1d_op Activation1d (alias_free_torch/act.py:23-27: up-FIR x2 -> SnakeBeta -> down-FIR)
 //                   of the fp32 (B, T, C) tensor, written straight in MFMA operand format: fp16, or
-//                   bf16 hi/lo planes for the bf16x3 split, channels padded to Cp = round_up(C, 32);
+//                   bf16 hi/lo planes for the bf16x3 split, channels padded to Cp = round_up(C, 32)
+//                   (act_mfma_kernel / act_coop_kernel in alcm_act.hip);
 //   opconv_kernel   implicit-GEMM conv1d on those planes: per 32-channel chunk the input window
 //                   rows [t0 - pad, t0 + BM + (k-1)d - pad) are copied once into LDS (double-buffered
 //                   across chunks) and reused by all k taps; the packed weight tile of each (chunk, tap)
@@ -25,71 +26,6 @@ namespace alcm {
 
 int act_coop(const float* x, void* const* y, int nset, int B, int T, int C, int Cp, const float* const* alpha_exp,
              const float* const* inv_beta, const Taps12O& f, int prec, hipStream_t s);
-
-// sin(x)^2: Cody-Waite quadrant reduction + minimax sin/cos on |r| <= pi/4 (~1 ulp, branch-free)
-__device__ __forceinline__ float op_sin_sq(float x) {
-  const float k = rintf(x * 0.63661977236758134f);
-  float r = fmaf(-k, 1.5703125f, x);
-  r = fmaf(-k, 4.837512969970703125e-4f, r);
-  r = fmaf(-k, 7.54978995489188216e-8f, r);
-  const float z = r * r;
-  const float sn = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
-  const float cs = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                                  4.166664568298827e-2f), z, -0.5f), z, 1.0f);
-  const float v = (((int)k) & 1) ? cs : sn;
-  return v * v;
-}
-
-// ------------------------------------------------------------------ Activation1d -> operand planes
-// thread = (batch, run of AOP_R output rows, channel pair): two channels ride in one float2 so the FIR
-// FMAs issue as v_pk_fma_f32 (half the VALU instructions of a scalar channel); lanes run along channel
-// pairs (8-byte coalesced loads, 4-byte stores of two 16-bit operands).  SnakeBeta's sin^2(z) is
-// 1/2 - cos(2z)/2 with 2z reduced to [-1/2, 1/2] revolutions and the hardware v_cos_f32 (a handful of
-// instructions instead of a ~20-op polynomial).  Pairs at or beyond C write zeros (operand padding).
-constexpr int AOP_R = 16;  // output rows per thread
-
-// thread = (batch, run of R output rows, channel pair); lanes run along channel pairs (8-byte coalesced
-// loads, 4-byte stores).  R trades halo work ((2R+10)/R upsampled samples per output) against registers
-// (occupancy): the FIR/snake chains are dependency-bound, so more resident waves matter.
-template <int PREC, int R>
-__global__ __launch_bounds__(256) void act_op_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t y_lo,
-                                                     int T, int C, int Cp, const float* __restrict__ aexp,
-                                                     const float* __restrict__ ibeta, const Taps12O f,
-                                                     uint32_t total, FastDiv pdiv, FastDiv rdiv) {
-  constexpr float INV_PI = 0.318309886183790671538f;
-  for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < total; w += gridDim.x * 256u) {
-    uint32_t rb, cpair, b, run;
-    pdiv.divmod(w, rb, cpair);
-    rdiv.divmod(rb, b, run);
-    const int c = 2 * (int)cpair;
-    const int j0 = (int)run * R;
-    u16* yb = y + ((int64_t)b * T) * Cp + c;
-    if (c >= C) {  // operand padding channels
-      for (int r = 0; r < R && j0 + r < T; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, f32x2{0.f, 0.f});
-      continue;
-    }
-    const float* xb = x + ((int64_t)b * T) * C + c;
-    const f32x2 ear = f32x2{aexp[c], aexp[c + 1]} * INV_PI;
-    const f32x2 h = f32x2{ibeta[c], ibeta[c + 1]} * 0.5f;
-    if (j0 >= 6 && j0 + R + 6 <= T) {
-      f32x2 win[R + 12];
-#pragma unroll
-      for (int i = 0; i < R + 12; ++i) win[i] = *reinterpret_cast<const f32x2*>(xb + (int64_t)(j0 - 6 + i) * C);
-      f32x2 o[R];
-      act_run_interior<R>(win, f, ear, h, o);
-#pragma unroll
-      for (int r = 0; r < R; ++r) op_store2<PREC>(yb + (int64_t)(j0 + r) * Cp, y_lo, o[r]);
-    } else {
-      // sequence edges: replicate padding of the up (pad 5) and down (pad 5/6) filters
-      for (int j = j0; j < j0 + R && j < T; ++j) {
-        const f32x2 o = act_one_clamped(j, T, f, ear, h, [&](int i) {
-          return *reinterpret_cast<const f32x2*>(xb + (int64_t)i * C);
-        });
-        op_store2<PREC>(yb + (int64_t)j * Cp, y_lo, o);
-      }
-    }
-  }
-}
 
 // three Activation1d of one input with their own SnakeBeta parameters and the same FIR taps (a BigVGAN stage's three
 // resblocks' first half-layer): one cooperative pass, the input window loaded once (bit-identical to three calls)
@@ -154,18 +90,12 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
   if (C % 2) return set_error(ALCM_E_INVALID, "activation1d_op: C must be even");
   if (prec < PREC_BF16 || prec > PREC_F16W2) return set_error(ALCM_E_INVALID, "activation1d_op: bad prec");
   if ((((uintptr_t)x) & 7) || (((uintptr_t)y) & 3)) return set_error(ALCM_E_INVALID, "activation1d_op: alignment");
-  const int R = knobs().act_rows;  // diagnostics: rows per thread (8 or 16)
-  const int runs = (T + R - 1) / R;
-  const int64_t total = (int64_t)B * runs * (Cp / 2);
-  if (total >= (1ll << 31) || (int64_t)B * T * Cp >= (1ll << 40))
-    return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
+  if ((int64_t)B * T * Cp >= (1ll << 40)) return set_error(ALCM_E_INVALID, "activation1d_op: problem too large");
   Taps12O f;
   for (int k = 0; k < 12; ++k) {
     f.up[k] = 2.0f * up_filter[k];
     f.dn[k] = down_filter[k];
   }
-  const int64_t y_lo = (int64_t)B * T * Cp;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
   if (act_mfma_ok(C, Cp, prec) && !(((uintptr_t)x) & 15) && !(((uintptr_t)y) & 15)) {  // both FIRs on MFMA (alcm_act.hip): the wide stages under the mixed policy
     void* tok = prof_start(s);
     ALCM_TRY(act_mfma(x, false, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
@@ -176,38 +106,15 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
     }
     return 0;
   }
-  if (!knobs().act_v1) {  // LDS-cooperative kernel (alcm_act.hip); ALCM_ACT_V1=1: per-thread runs
-    void* tok = prof_start(s);
-    void* ys[1] = {y};
-    const float* ae[1] = {alpha_exp};
-    const float* ib[1] = {inv_beta};
-    ALCM_TRY(act_coop(x, ys, 1, B, T, C, Cp, ae, ib, f, prec, s));
-    if (tok) {
-      char name[64];
-      std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>", prec == PREC_F16W2 ? PREC_F16 : prec);
-      const double e = (double)B * T;
-      prof_stop(tok, s, name, 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
-    }
-    ALCM_HIP(hipGetLastError());
-    return 0;
-  }
+  // otherwise the LDS-cooperative kernel (alcm_act.hip)
   void* tok = prof_start(s);
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, x, (u16*)y, y_lo, T, C, Cp, alpha_exp, inv_beta, f,
-                       (uint32_t)total, FastDiv((uint32_t)(Cp / 2)), FastDiv((uint32_t)runs));
-  };
-  if (R == 16) {
-    if (prec == PREC_SPLIT) launch(act_op_kernel<PREC_SPLIT, 16>);
-    else if (prec == PREC_BF16) launch(act_op_kernel<PREC_BF16, 16>);
-    else launch(act_op_kernel<PREC_F16, 16>);
-  } else {
-    if (prec == PREC_SPLIT) launch(act_op_kernel<PREC_SPLIT, 8>);
-    else if (prec == PREC_BF16) launch(act_op_kernel<PREC_BF16, 8>);
-    else launch(act_op_kernel<PREC_F16, 8>);
-  }
+  void* ys[1] = {y};
+  const float* ae[1] = {alpha_exp};
+  const float* ib[1] = {inv_beta};
+  ALCM_TRY(act_coop(x, ys, 1, B, T, C, Cp, ae, ib, f, prec, s));
   if (tok) {
-    char name[96];
-    std::snprintf(name, sizeof(name), "alcm::act_op_kernel<%d, %d>", prec == PREC_F16W2 ? PREC_F16 : prec, R);
+    char name[64];
+    std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>", prec == PREC_F16W2 ? PREC_F16 : prec);
     const double e = (double)B * T;
     prof_stop(tok, s, name, 2.0 * 36.0 * e * C, e * (4.0 * C + 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
   }
@@ -232,7 +139,6 @@ struct OpConvDev {
   int tstride, tshift;  // tile i of a batch computes rows [i * tstride - tshift, + BM)
   ActEpiDev act;        // ACT: fused Activation1d epilogue into operand planes
   int act_prefetch;     // ACT: residual prefetched into registers before the K loop
-  int ablate;           // diagnostics (ALCM_OPCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA
   int ostride, ooff, orows;  // output row of conv row t: b * orows + t * ostride + ooff (a ConvTranspose phase)
 };
 
@@ -291,7 +197,7 @@ __global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvD
   // residual prefetch (narrow tiles): tile rows are one contiguous block of mrows * N floats
   float4 rp[RPER];  // dead (and eliminated) unless PRE
   // ACT tiles: the residual of every tile row (halo rows included) is loaded into registers before the K loop,
-  // so the epilogue does not stall on one dependent global load per float4 (ALCM_TAIL_PREFETCH=0: off, A-B)
+  // so the epilogue does not stall on one dependent global load per float4
   // (not in the ACT3 build: the 48 registers would spill)
   constexpr bool PREA_OK = ACT && !ACT3;
   constexpr int RPA = PREA_OK ? (BM * (BN / 4) + 255) / 256 : 1;
@@ -436,13 +342,6 @@ __global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvD
       bh[j] = *reinterpret_cast<const bf16x8*>(bh_base + b_off + j * 16 * 32);
       if (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(bl_base + b_off + j * 16 * 32);
     }
-    if (P.ablate & 2) {  // keep the fragment reads, skip the products
-#pragma unroll
-      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(ah[i]));
-#pragma unroll
-      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bh[j]));
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -487,15 +386,6 @@ __global__ __launch_bounds__(256, ACT3 ? 3 : 1) void opconv_kernel(const OpConvD
     if (g < SPC) step(cc, g, more, S0{});
   }
 
-  if (P.ablate & 1) {
-    float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (sum == 123.f && P.out) P.out[tid] = sum;
-    return;
-  }
   // epilogue
   if constexpr (ACT) {
     // v = conv + bias (+ res) for every tile row inside [0, T) -> LDS; fp32 out (if any) for the rows this
@@ -698,7 +588,6 @@ static int tile_variant(int prec) {
 }
 
 bool opconv_act_supported(int prec, int N, int Cp_in) {
-  if (knobs().no_act_fusion) return false;  // diagnostics / A-B
   if (N % 4 || N <= 0) return false;
   // opconv_kernel ACT tiles (BN <= 96): HBM-bound layers, the fusion saves ~15%.  Wide layers keep conv + standalone
   // Activation1d: a fused epilogue in the two-workgroup wide conv measured -6 % end to end
@@ -754,8 +643,7 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   P.w_lo = a.w_lo_off; P.kpad = a.kpad; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_act = a.out_act; P.accumulate = a.accumulate;
   P.out_scale = a.out_scale;
-  P.act_prefetch = knobs().tail_prefetch;
-  P.ablate = knobs().opconv_ablate;
+  P.act_prefetch = 1;
   P.ostride = strided ? a.out_stride : 1;
   P.ooff = strided ? a.out_offset : 0;
   P.orows = strided ? a.out_rows : a.T;

@@ -265,7 +265,7 @@ int split_planes(const float* x, int64_t rows, int C, int T, const float* scale,
   return 0;
 }
 
-bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K && knobs().sgemm; }
+bool sgemm_planes_ok(int K, int N, int kpad) { return K % 32 == 0 && N % SG_BN == 0 && kpad >= K; }
 
 // 1x1 conv / linear on one operand plane (ALCM_LIN1: 1 = 32-deep stages in a 4-deep ring, 2 = 64-deep stages double-
 // buffered, 0 = off: wconv2, -1 = by shape: the 64-deep build for plane outputs only).  Measured per step at B = 32

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
 // resident-weight kernel (one workgroup per CU at C >= 48) cannot do.  Ring slot layout: row n of 64 B (32 fp16 of
 // K), its 16-B piece q at physical piece q ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows).
 template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
-__global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TConvDev P) {
+__global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
   constexpr int NT = 256, RPW = BM / 4, TM = RPW / 16;
   constexpr int NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
   constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TC
   constexpr int STAGE = BM * OTS * 4;
   constexpr int REGION = (STAGE > WINB + RINGB ? STAGE : WINB + RINGB);
   constexpr int SMEM = REGION + 1024 * 4;               // + one scratch KB per wave for padding DMA instructions
-  static_assert(SMEM <= (BM <= 128 ? 54 * 1024 : 81920), "two (BM = 128: three) workgroups per CU");
+  static_assert(SMEM <= 81920, "two workgroups per CU");
   static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
   static_assert(C % 8 == 0 && NS % 4 == 0 && RPW % 16 == 0, "geometry");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, BM <= 128 ? 3 : 2) void tconv2_kernel(const TC
   const int K = P.ksize, dil = P.dil;
   const int nslice = P.kd / 32;
   const int E = BM - 2 * ACT_EPI_HALO;
-  // persistent grid (ALCM_TCONV_STAGGER >= 1): the second half of the workgroups (the second workgroup of each CU)
+  // persistent grid (C = 96): the second half of the workgroups (the second workgroup of each CU)
   // starts P.stagger sleeps late, so the two workgroups of a CU alternate K loop (MFMA) and Activation1d epilogue
   // (VALU) instead of running both phases in lockstep
   if (P.stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
@@ -503,8 +503,7 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   const int tk = knobs().tconv;
   // measured per launch (scripts/microbench.py tconv): streamed wins at C = 96 and C = 24, resident at C = 48
   const bool streamed = tk == 2 || (tk != 3 && C != 48);
-  const bool small = streamed && C != 96 && knobs().tconv_bm == 128;  // 128-row tiles, three workgroups per CU
-  const int BM = small ? 128 : (C == 96 ? 192 : 256);
+  const int BM = C == 96 ? 192 : 256;
   const int NS = (!streamed && C == 96) ? 48 : C;
   P.ncg = a.N / NS;
   P.tiles_per_batch = (a.T + (BM - 2 * ACT_EPI_HALO) - 1) / (BM - 2 * ACT_EPI_HALO);
@@ -515,26 +514,19 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   void* tok = prof_start(s);
   int rc;
   if (streamed) {
-    // ALCM_TCONV_STAGGER: 0 = one workgroup per tile; >= 1 = persistent, two (BM 128: three) workgroups per CU, the
-    // second half delayed by stagger - 1 sleeps; -1 (default) by shape: C = 96 persistent with 2 sleeps (scripts/
-    // microbench.py tconv, one box: k11 0.547 -> 0.491 ms, k3 0.300 -> 0.301, conv2 + residual 0.732 -> 0.695), C = 24
-    // one workgroup per tile (persistent measured +5..+17 %)
+    // C = 96: persistent, two workgroups per CU, the second half delayed by 2 sleeps (scripts/microbench.py tconv, one
+    // box: k11 0.547 -> 0.491 ms, k3 0.300 -> 0.301, conv2 + residual 0.732 -> 0.695); C = 24 one workgroup per tile
+    // (persistent measured +5..+17 %)
     int grid2 = (int)nt;
-    const int stg = knobs().tconv_stagger >= 0 ? knobs().tconv_stagger : (C == 96 ? 3 : 0);
+    const int stg = C == 96 ? 3 : 0;
     if (stg > 0) {
       int dev = 0, ncu = 256;
       if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * (small ? 3 : 2));
+      grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * 2);
       P.stagger = stg - 1;
     }
     if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11>(P, grid2, act, a.res, outw, acc_mode, s);
-    else if (small && C == 48) {
-      if (npb == 2) rc = tc2_mode<48, 48, 2, 128, 14>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<48, 48, 1, 128, 14>(P, grid2, act, a.res, outw, acc_mode, s);
-    } else if (small) {
-      if (npb == 2) rc = tc2_mode<24, 24, 2, 128, 7>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 128, 7>(P, grid2, act, a.res, outw, acc_mode, s);
-    } else if (C == 48) {
+    else if (C == 48) {
       if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
       else rc = tc2_mode<48, 48, 1, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
     } else {
@@ -546,7 +538,7 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     // tile it takes (tile % ncg == blockIdx % ncg); C = 24 fits two per CU
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int wgs = knobs().tconv_wgs > 0 ? knobs().tconv_wgs : (C == 24 ? 2 : 1);
+    const int wgs = C == 24 ? 2 : 1;
     int grid = std::min<int64_t>(nt, (int64_t)ncu * wgs);
     grid = std::max(P.ncg, grid / P.ncg * P.ncg);
     if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);

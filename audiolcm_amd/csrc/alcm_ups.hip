@@ -189,7 +189,7 @@ __global__ __launch_bounds__(512, (UpsGeo<CP, NOUT>::OCC)) void ups2_kernel(cons
 
 // ------------------------------------------------------------------------------------------------------ host
 bool ups2_supported(int cin, int cout, int cpad, int rate, int taps) {
-  if (!knobs().ups2 || rate != 2 || taps != 2) return false;
+  if (rate != 2 || taps != 2) return false;
   return (cin == 96 && cpad == 96 && cout == 48) || (cin == 48 && cpad == 48 && cout == 24);
 }
 

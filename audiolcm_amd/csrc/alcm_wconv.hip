@@ -659,8 +659,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if (nt >= (1ll << 30) || (int64_t)a.B * a.T * a.Cp >= (1ll << 40) || (int64_t)a.B * a.T * a.N >= (1ll << 40)) return 0;
   if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
   P.nwg = (int)nt;
-  const int ord = knobs().wconv_order;
-  P.n_major = ord >= 0 ? ord : 1;
+  P.n_major = 1;
   const int R = (P.nwg + 7) / 8;
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
@@ -678,7 +677,7 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   return 1;
 }
 
-// wconv2 tile by shape (ALCM_WCONV_TILE = -1): 256 x 96 where the weight stream dominates the per-CU fetch (k >= 7:
+// wconv2 tile by shape: 256 x 96 where the weight stream dominates the per-CU fetch (k >= 7:
 // the window is amortised over >= 7 taps) and there is at least one 256-row tile per CU; 128 x 192 elsewhere.
 // Measured per launch (B = 32, one box): s0 C768 k11 0.946 -> 0.860 ms, s1 C384 k11
 // 0.973 -> 0.934, s2 C192 k11 0.583 -> 0.559, DiT FFN-down 0.377 -> 0.358; k3 shapes equal or slower (VAE k3 +17 %)
@@ -729,9 +728,8 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   auto al16 = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!(al16(a.bias) && al16(a.res) && al16(a.out))) return 0;
   if (a.geglu_plane && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
-  // wconv2 tile (ALCM_WCONV_TILE): 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
-  const int tk = knobs().wconv_tile;
-  const bool t256 = !ragged && (tk >= 0 ? tk == 1 : wconv2_tile256(a));
+  // wconv2 tile: 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
+  const bool t256 = !ragged && wconv2_tile256(a);
   const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
   if (a.N % BN2 == 0 || ragged) {
     WConvDev P{};
@@ -749,10 +747,9 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     // an XCD's weight slice: that XCD's N tiles stay in its L2 (C768 k11 -17 %, DiT FFN -3..-10 %); M-major
     // elsewhere (the N tiles of an M tile share its input window in L2)
     const int tiles_m = a.B * ((a.T + BM2 - 1) / BM2);
-    const int ord = knobs().wconv_order;
     // (the GEGLU up-projection, 64 M tiles x 48 N tiles of 1 MB weight slices: N-major -4 %, its M-major order
     // re-reads the weights from the Infinity Cache once per M tile, 3 GB counted per launch)
-    P.n_major = ord >= 0 ? ord : (a.Cp * a.ksize >= 4096 && (tiles_m >= 128 || (a.geglu_plane && tiles_m >= 64)));
+    P.n_major = (a.Cp * a.ksize >= 4096 && (tiles_m >= 128 || (a.geglu_plane && tiles_m >= 64)));
     P.tiles_per_batch = (a.T + BM2 - 1) / BM2;
     P.tiles_n = (a.N + BN2 - 1) / BN2;
     const int64_t nwg2 = (int64_t)a.B * P.tiles_per_batch * P.tiles_n;

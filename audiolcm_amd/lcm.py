@@ -16,7 +16,6 @@ Differences from the reference that are deliberate and documented in DESIGN.md:
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -145,8 +144,6 @@ class LCM_audio:
 def _h2d(t: torch.Tensor, dev) -> torch.Tensor:
     """Host tensor -> device through the pinned caching allocator, asynchronously on the current stream (the pinned
     block stays reserved until the copy has run)."""
-    if os.environ.get("ALCM_SYNC_H2D"):  # (temporary A/B: the blocking pageable copy)
-        return t.to(dev)
     return t.pin_memory().to(dev, non_blocking=True)
 
 

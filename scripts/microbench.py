@@ -68,27 +68,6 @@ def bench_act(B=32):
         print(f"act1d C={C} T={T}: {ms:.3f} ms {B * T * C * 8 / 1e9 / ms:.2f} TB/s")
 
 
-def bench_actnp(B=32):
-    """cooperative Activation1d -> operand planes: 32-channel vs 64-channel tiles (ALCM_ACT_NP 16 / 32)"""
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    for C, T, p in ((768, 2496, 2), (384, 9984, 2), (192, 19968, 2), (192, 19968, 1)):
-        x = torch.randn((B, T, C), device="cuda")
-        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
-        npl = 2 if p == 1 else 1
-        gb = B * T * C * (4 + 2 * npl) / 1e9
-        line, outs = [], []
-        for v in os.environ.get("ACT_NP", "16,32").split(","):
-            os.environ["ALCM_ACT_NP"] = v
-            _hip.reload_knobs()
-            ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p), reps=10)
-            outs.append(K.activation1d_op(x, a, bt, f, f, p).clone())
-            line.append(f"np{v} {ms:7.3f} ms {gb / ms:5.2f} TB/s")
-        os.environ.pop("ALCM_ACT_NP")
-        _hip.reload_knobs()
-        same = all(torch.equal(outs[0], o) for o in outs[1:])
-        print(f"act_op C={C:3d} prec={p}: " + " | ".join(line) + f" | identical {same}", flush=True)
-
-
 def bench_conv_one(B=32, T=9984, C=384, k=7, d=3, split=True):
     """single window-conv configuration (target for rocprofv3 --pmc passes)"""
     x = torch.randn((B, T, C), device="cuda")
@@ -111,11 +90,8 @@ def bench_op(B=32):
             npl = 2 if p == 1 else 1
             cp = (C + 31) // 32 * 32
             gb = B * T * (C * 4 + cp * 2 * npl) / 1e9
-            for rows in ("8", "16"):
-                os.environ["ALCM_ACT_ROWS"] = rows
-                _hip.reload_knobs()
-                ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p))
-                print(f"act_op C={C:3d} prec={p} rows={rows}: {ms:7.3f} ms {gb / ms:6.2f} TB/s", flush=True)
+            ms = timeit(lambda: K.activation1d_op(x, a, bt, f, f, p))
+            print(f"act_op C={C:3d} prec={p}: {ms:7.3f} ms {gb / ms:6.2f} TB/s", flush=True)
             pl = K.activation1d_op(x, a, bt, f, f, p)
             for k, d in ((11, 5), (7, 3), (3, 1)):
                 w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
@@ -280,49 +256,14 @@ def bench_tail(B=32):
             w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
             pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
             line = []
-            for v in [f"{n}/{pf}" for n in os.environ.get("NCONV_VARS", "0,1").split(",")
-                      for pf in os.environ.get("PF_VARS", "1").split(",")]:
-                v, pf = v.split("/")
-                os.environ["ALCM_TAIL_PREFETCH"] = pf
-                os.environ["ALCM_NCONV"] = v.split(":")[0]
+            for v in os.environ.get("NCONV_VARS", "0,1").split(","):
+                os.environ["ALCM_NCONV"] = v
                 _hip.reload_knobs()
-                if ":" in v:
-                    os.environ["ALCM_NCONV_NB"] = v.split(":")[1]
-                    _hip.reload_knobs()
-                else:
-                    os.environ.pop("ALCM_NCONV_NB", None)
-                    _hip.reload_knobs()
                 ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
                 ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
                 ms3 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw))
-                line.append(f"v{v}pf{pf}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
+                line.append(f"nconv{v}: act {ms1:6.3f} res+act {ms2:6.3f} res {ms3:6.3f}")
             os.environ.pop("ALCM_NCONV")
-            _hip.reload_knobs()
-            print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
-
-
-def bench_tailab(B=32):
-    """timing ablations of the tail convs as the model runs them (ALCM_OPCONV_ABLATE: 1 no epilogue, 2 no MFMA,
-    3 neither): conv1 + fused Activation1d, conv2 + residual + fused Activation1d, per tail stage, k = 11 / 3"""
-    from audiolcm_amd.recipe import kaiser_sinc_filter1d
-    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    for C, T, p in ((96, 39936, 2), (48, 79872, 3), (24, 159744, 3)):  # mixed-policy precisions
-        x = torch.randn((B, T, C), device="cuda")
-        r = torch.randn((B, T, C), device="cuda")
-        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
-        pl = K.operand_planes(x, p)
-        cp = (C + 31) // 32 * 32
-        for k, d in ((11, 5), (3, 1)):
-            w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
-            pw = K.pack_conv_weight(torch.nn.functional.pad(w, (0, 0, 0, cp - C)).contiguous())
-            line = []
-            for ab in os.environ.get("ABLATE", "0,1,2,3").split(","):
-                os.environ["ALCM_OPCONV_ABLATE"] = ab
-                _hip.reload_knobs()
-                ms1 = timeit(lambda: K.opconv(pl, C, w, None, d, p, packed=pw, act=(a, bt, f, f), fp32_out=False))
-                ms2 = timeit(lambda: K.opconv(pl, C, w, None, d, p, residual=r, packed=pw, act=(a, bt, f, f)))
-                line.append(f"ab{ab}: conv1+act {ms1:6.3f} conv2+res+act {ms2:6.3f}")
-            os.environ.pop("ALCM_OPCONV_ABLATE")
             _hip.reload_knobs()
             print(f"tail C={C:3d} k={k:2d} d={d} prec={p}: " + " | ".join(line), flush=True)
 
@@ -473,4 +414,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "tailab": bench_tailab, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "actnp": bench_actnp, "conv1": bench_conv_one}[w]()
+        {"xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
