@@ -215,9 +215,11 @@ __device__ __forceinline__ void act_epilogue_tile(const float* tile, int ots, in
 // act_epilogue_tile with the channel pairs NP of the tile known at compile time and no operand-padding work (the
 // caller's planes keep their padding channels, which no consumer reads): work item w = (run, pair) by a constant
 // division, the caller picks R so that NP * runs ~ its thread count (one pass)
-template <int PREC, int R, int NP>
+template <int PREC, int R, int NP, bool NOSTORE = false>
 __device__ __forceinline__ void act_epilogue_ct(const float* tile, int ots, int trow0, int e_lo, int e_hi, int T,
                                                 int c0, int b, const ActEpiDev& A, int tid, int nthr) {
+  // NOSTORE (timing ablation only, results wrong): the plane stores replaced by a never-taken dependent store
+  f32x2 sink = f32x2{0.f, 0.f};
   constexpr float INV_PI = 0.318309886183790671538f;
   const int nrun = (e_hi - e_lo + R - 1) / R;
   // the batch's plane base is uniform; per-item byte offsets stay 32-bit (a batch's plane is < 4 GB), so the stores
@@ -239,16 +241,22 @@ __device__ __forceinline__ void act_epilogue_ct(const float* tile, int ots, int 
       f32x2 o[R];
       act_run_interior<R>(win, A.f, ear, h, o);
 #pragma unroll
-      for (int r = 0; r < R; ++r) op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o[r]);
+      for (int r = 0; r < R; ++r) {
+        if constexpr (NOSTORE) sink += o[r];
+        else op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o[r]);
+      }
     } else {
       for (int r = 0; r < jn; ++r) {
         const f32x2 o = act_one_clamped(j0 + r, T, A.f, ear, h, [&](int i) {
           return *reinterpret_cast<const f32x2*>(col + (i - trow0) * ots);
         });
-        op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o);
+        if constexpr (NOSTORE) sink += o;
+        else op_store2<PREC>(reinterpret_cast<u16*>(pb + (yo + r * ys)), A.plane_lo, o);
       }
     }
   }
+  if constexpr (NOSTORE)
+    if (sink.x == 123.f && sink.y == 321.f) op_store2<PREC>(reinterpret_cast<u16*>(pb), A.plane_lo, sink);
 }
 
 }  // namespace alcm

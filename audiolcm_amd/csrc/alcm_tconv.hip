@@ -49,8 +49,32 @@ struct TConvDev {
   int tiles_per_batch, ntiles, ncg;  // ncg: column groups (N / NS)
   int wslots;         // 16-B slots per LDS weight row (odd)
   int ablate;         // diagnostics (ALCM_TCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA,
-                      // 4 no window DMA
+                      // 4 no window DMA, 8 no plane stores, 16 no fp32 state stores
   int stagger;        // tconv2: s_sleep(127) count before the second half of a persistent grid starts
+  unsigned long long* trace;  // diagnostics (ALCM_XP3 = 1): per-phase shader-clock sums over waves and tiles, or null
+};
+
+// phase timer of the diagnostics trace: wave-uniform shader-clock stamps, summed per phase over the tiles of a wave
+// and added to P.trace by lane 0 at the end (vector atomics)
+struct TcTimer {
+  bool on;
+  unsigned long long last, ph[8];
+  __device__ __forceinline__ void init(bool enable) {
+    on = enable;
+    for (int i = 0; i < 8; ++i) ph[i] = 0;
+    last = on ? __builtin_readcyclecounter() : 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    if (!on) return;
+    const unsigned long long t = __builtin_readcyclecounter();
+    ph[i] += t - last;
+    last = t;
+  }
+  __device__ __forceinline__ void flush(unsigned long long* out) {
+    if (!on || (threadIdx.x & 63)) return;
+    unsigned long long* o = out + (blockIdx.x & 63) * 8;  // 64 slot sets: no single-address contention
+    for (int i = 0; i < 8; ++i) atomicAdd(o + i, ph[i]);
+  }
 };
 
 __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
@@ -65,7 +89,7 @@ template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, boo
           bool PRE = true>
 __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const float (&bias_r)[TN],
                                           const float4 (&rv)[PRE ? NRES : 1], float* ot, int wr0, int t0, int e0, int E,
-                                          int b, int n0, const TConvDev& P) {
+                                          int b, int n0, const TConvDev& P, TcTimer& tm) {
   constexpr int OTS = NS + 4;
   const int tid = threadIdx.x, lane = tid & 63, q4 = lane >> 4, l16 = lane & 15;
   // v = conv + bias -> LDS
@@ -80,7 +104,22 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
         if (n < NS) ot[m * OTS + n] = acc[i][j][r] + bias_r[j];
       }
     }
+  // residual rows not prefetched before the K loop (C = 96: 18 float4 per thread, too many registers beside the
+  // accumulators): every load issued here in one burst, once the accumulators are dead, so the loop below waits for
+  // one round trip (one load per iteration, next to the state stores that may alias it, waited for 18 round trips:
+  // C96 k3 conv2 + residual + Activation1d 0.59 -> 0.46 ms, scripts/microbench.py tphase)
+  constexpr bool LATE = RES && !PRE;
+  float4 rl[LATE ? NRES : 1];
+  if constexpr (LATE) {
+#pragma unroll
+    for (int i = 0; i < NRES; ++i) {
+      const int e = min(tid + i * NT, BM * (NS / 4) - 1);
+      const int m = e / (NS / 4), n = (e - m * (NS / 4)) * 4;
+      rl[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + min(max(t0 + m, 0), P.T - 1)) * P.N + n0 + n);
+    }
+  }
   __syncthreads();
+  tm.mark(3);
   const int e_hi = min(e0 + E, P.T);
   if constexpr (RES || OUTW || ACC) {
     // + residual (all tile rows: the activation reads the halo rows too); fp32 state of the owned rows
@@ -94,11 +133,11 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
       if constexpr (RES) {
         float4 r4;
         if constexpr (PRE) r4 = rv[PRE ? i : 0];
-        else r4 = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + min(max(t, 0), P.T - 1)) * P.N + n0 + n);
+        else r4 = rl[LATE ? i : 0];
         v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
         if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
       }
-      if ((OUTW || ACC) && t >= e0 && t < e_hi) {
+      if ((OUTW || ACC) && t >= e0 && t < e_hi && !(P.ablate & 16)) {
         float* op = P.out + ((int64_t)b * P.T + t) * P.N + n0 + n;
         if constexpr (ACC) {
           v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
@@ -112,8 +151,12 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
     }
     if constexpr (ACT) __syncthreads();
   }
-  if constexpr (ACT)
-    act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+  tm.mark(4);
+  if constexpr (ACT) {
+    if (P.ablate & 8) act_epilogue_ct<PREC_F16, R, NS / 2, true>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+    else act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+  }
+  tm.mark(5);
 }
 
 // C input channels, NS output channels per tile, NPB weight planes (1 = F16, 2 = F16W2), BM rows per tile,
@@ -172,6 +215,8 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
 
+  TcTimer tm;
+  tm.init(P.trace != nullptr);
   for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
     const int mt = tile / P.ncg;
     const int b = mt / P.tiles_per_batch;
@@ -201,6 +246,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    tm.mark(0);
 
     // ---- barrier-free K loop over 32-deep slices of the dense K
     f32x4 acc[TM][TN];
@@ -246,7 +292,9 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
       slice(s + 1);
     }
     if (s < nslice) slice(s);
+    tm.mark(1);
     __syncthreads();  // every window read retired: the region becomes the staged tile
+    tm.mark(2);
     if (P.ablate & 1) {
       float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
 #pragma unroll
@@ -257,9 +305,12 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
       continue;
     }
 
-    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P);
+    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
     __syncthreads();  // staged-tile reads retired before the next window DMA overwrites the region
+    tm.mark(6);
+    if (tm.on) tm.ph[7] += 1;
   }
+  tm.flush(P.trace);
 }
 
 // Streamed-weight variant (ALCM_TCONV=2 / by shape): 4 waves of 64 rows x NS columns, the weights of each 32-deep K
@@ -269,6 +320,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
 // K), its 16-B piece q at physical piece q ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows).
 template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
 __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
+  constexpr int PD = 2;  // weight slices in flight ahead of the one consumed (3: equal, the K loop is LDS-read bound)
   constexpr int NT = 256, RPW = BM / 4, TM = RPW / 16;
   constexpr int NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
   constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;
@@ -305,6 +357,8 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
   // (VALU) instead of running both phases in lockstep
   if (P.stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
     for (int i = 0; i < P.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  TcTimer tm;
+  tm.init(P.trace != nullptr);
   for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
   const int mt = tile / P.ncg, cg = tile - mt * P.ncg;
   const int n0 = cg * NS;
@@ -318,7 +372,9 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
   constexpr int NRES = (BM * (NS / 4) + NT - 1) / NT;
-  constexpr bool PRE = NRES <= 12;  // residual prefetched into registers (C = 96: loaded in the epilogue)
+  // residual prefetched into registers at the tile start (C = 96: loaded in the epilogue; prefetched, its 72 registers
+  // beside the accumulators spill and the window wait covers it: 0.59 -> 0.75 ms)
+  constexpr bool PRE = NRES <= 12;
   float4 rv[PRE ? NRES : 1];
   if constexpr (RES && PRE) {
 #pragma unroll
@@ -356,15 +412,23 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
       tc_glds16(src, i < SPI ? dst + i * 1024 : scratch + wave * 1024);
     }
   };
-  stage_slice(0);
-  if (nslice > 1) stage_slice(1);
-  if (nslice > 1) {
-    if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  static_assert(DPW <= 2, "vmcnt immediates below");
+  // wait until at most `ahead` slices' DMA are outstanding (every older access of this wave has landed)
+  auto wait_ahead = [&](int ahead) {
+    if (ahead >= 2) {
+      if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    } else if (ahead == 1) {
+      if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+  };
+  for (int j = 0; j < PD && j < nslice; ++j) stage_slice(j);
+  wait_ahead(min(PD, nslice) - 1);
   __builtin_amdgcn_s_barrier();
+  tm.mark(0);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -374,8 +438,7 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
   const char* arow = win + (wr0 + l16) * RS;
   const int bsw = (l16 >> 2) & 3;
   for (int s = 0; s < nslice; ++s) {
-    const bool more = s + 2 < nslice;
-    if (more) stage_slice(s + 2);
+    if (s + PD < nslice) stage_slice(s + PD);
     const int kk = s * 32 + q4 * 8;
     int tap = kk / C;
     const int c = kk - tap * C;
@@ -405,15 +468,12 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
         }
       __builtin_amdgcn_s_setprio(0);
     }
-    // slice s + 1 (issued one slice earlier) has landed; slice s + 2 stays in flight across the barrier
-    if (more) {
-      if constexpr (DPW == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
+    // slice s + 1 has landed; the slices issued beyond it stay in flight across the barrier
+    wait_ahead(min(PD - 1, nslice - 2 - s));
     __builtin_amdgcn_s_barrier();
   }
+  tm.mark(1);
+  tm.mark(2);
   if (P.ablate & 1) {
     float sum = 0.f;
 #pragma unroll
@@ -423,12 +483,17 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
     if (sum == 123.f && P.out) P.out[tid] = sum;
     continue;
   }
-  tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P);
+  tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
   __syncthreads();  // staged-tile reads retired before the next tile's DMA overwrites the region
+  tm.mark(6);
+  if (tm.on) tm.ph[7] += 1;
   }
+  tm.flush(P.trace);
 }
 
 // -------------------------------------------------------------------------------------------------- host
+unsigned long long* g_tc_trace = nullptr;  // diagnostics trace buffer (8 sums), allocated on first use
+
 struct TConvCfg {
   int C, NS, NPB, BM;
 };
@@ -495,6 +560,13 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   if (act) P.act = *act;
   P.ablate = knobs().tconv_ablate;
+  if (knobs().xp[3] == 1) {
+    if (!g_tc_trace) {
+      ALCM_HIP(hipMalloc(&g_tc_trace, 512 * sizeof(unsigned long long)));
+      ALCM_HIP(hipMemset(g_tc_trace, 0, 512 * sizeof(unsigned long long)));
+    }
+    P.trace = g_tc_trace;
+  }
   const int slots = kd / 8;
   P.wslots = slots % 2 ? slots : slots + 1;
   const int npb = a.prec == PREC_F16W2 ? 2 : 1;
@@ -591,4 +663,22 @@ extern "C" int alcm_opconv_dense(const alcm_opconv_args* args, alcm_stream_t str
                        (act ? M * a.N * 2.0 : 0.0);
   return tconv(a, (const u16*)a.w + 2 * a.w_lo_off, a.w_lo_off, a.kpad, act ? &E : nullptr, flops, bytes,
                (hipStream_t)stream);
+}
+
+// diagnostics: the tconv phase trace (ALCM_XP3 = 1) summed since the last reset; reset zeroes it (stream-ordered on
+// the null stream)
+extern "C" int alcm_debug_tconv_trace(unsigned long long* out8, int reset) {
+  if (!alcm::g_tc_trace) {
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    return 0;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  unsigned long long h[512];
+  if (hipMemcpy(h, alcm::g_tc_trace, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  for (int i = 0; i < 8; ++i) {
+    out8[i] = 0;
+    for (int j = 0; j < 64; ++j) out8[i] += h[j * 8 + i];
+  }
+  if (reset && hipMemset(alcm::g_tc_trace, 0, sizeof(h)) != hipSuccess) return -1;
+  return 0;
 }

@@ -328,6 +328,48 @@ def bench_tail1d(B=32):
     torch.cuda.synchronize()
 
 
+def bench_tphase(B=32):
+    """per-phase shader-clock breakdown of the tail convs as the model runs them (ALCM_XP3=1 trace): cycles per tile
+    per wave of [window + first slices, K loop, post-loop barrier, stage v, residual + fp32 out, Activation1d, final
+    barrier]; TCONFIGS = C:k:mode,... (mode conv1 / conv2)"""
+    import ctypes
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    L = _hip.lib()
+    out8 = (ctypes.c_ulonglong * 8)()
+    os.environ["ALCM_XP3"] = "1"
+    _hip.reload_knobs()
+    cfgs = os.environ.get("TCONFIGS", "96:3:conv2,96:11:conv2,96:11:conv1,48:3:conv2,48:11:conv2,24:3:conv2,24:11:conv2")
+    for cfg in cfgs.split(","):
+        C, k, mode = int(cfg.split(":")[0]), int(cfg.split(":")[1]), cfg.split(":")[2]
+        T = {96: 39936, 48: 79872, 24: 159744}[C]
+        d, p = (5 if k == 11 else 1), (2 if C == 96 else 3)
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        pl = K.operand_planes(x, p)
+        w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+        pd = K.pack_conv_weight(w)
+        conv2 = mode == "conv2"
+        run = lambda: K.opconv(pl, C, w, None, d, p, residual=r if conv2 else None, packed=pd, act=(a, bt, f, f),
+                               fp32_out=conv2, dense=True)
+        for xv in os.environ.get("XP_VALS", "0").split(","):
+            os.environ[os.environ.get("XP_NAME", "ALCM_XP0")] = xv
+            _hip.reload_knobs()
+            run()
+            L.alcm_debug_tconv_trace(out8, 1)
+            ms = timeit(run, reps=5)
+            L.alcm_debug_tconv_trace(out8, 1)
+            v = list(out8)
+            tiles = max(v[7], 1)
+            ph = " ".join(f"{x / tiles:7.0f}" for x in v[:7])
+            print(f"tphase C={C:3d} k={k:2d} {mode} xp={xv}: {ms:6.3f} ms  cycles/tile/wave [win kloop bar stage res act "
+                  f"bar] {ph}  sum {sum(v[:7]) / tiles:7.0f}  wave-tiles {v[7]}", flush=True)
+        os.environ.pop(os.environ.get("XP_NAME", "ALCM_XP0"))
+    os.environ.pop("ALCM_XP3")
+    _hip.reload_knobs()
+
+
 def bench_tail1(B=32):
     """3 launches of the stage-4 (C = 48, k = 11, d = 5, F16W2) conv2 + residual + fused Activation1d as the model
     runs it, with the current ALCM_* settings (target of rocprofv3 --pmc passes)"""
@@ -414,4 +456,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
+        {"tphase": bench_tphase, "xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
