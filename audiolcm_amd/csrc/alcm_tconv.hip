@@ -159,11 +159,54 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
   tm.mark(5);
 }
 
+// one wave's LDS-DMA of a tile window through a buffer descriptor over the batch's plane rows (device-only: the
+// buffer builtins inside a kernel lambda make the host pass drop the kernel's launch stub): slot i of this lane at
+// byte offset off[i] + shift, out-of-range offsets (before row 0, past the batch, or the 0x7fffffff of an unused
+// slot) land as zeros without a memory access
+template <int I0, int I1, int N>
+__device__ __forceinline__ void tc_window_dma(uintptr_t base, uint32_t bytes, __attribute__((address_space(3))) char* dst,
+                                              const uint32_t (&off)[N], uint32_t shift) {
+  // descriptor from provably wave-uniform scalars (readfirstlane of the base halves and the size)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uintptr_t)hi << 32) | lo), 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+#pragma unroll
+  for (int i = I0; i < I1; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + i * 1024), 16, off[i] + shift, 0, 0, 0);
+}
+
+// the loader's window DMA of one tile (rows [t0 - pad, t0 - pad + WR) of its batch), slots [I0, I1)
+template <int I0, int I1, int N>
+__device__ __forceinline__ void tc_window_tile(const TConvDev& P, int tile, int E, uint32_t batch_bytes,
+                                               __attribute__((address_space(3))) char* dst, const uint32_t (&off)[N]) {
+  if (P.ablate & 4) return;
+  const int mt = tile / P.ncg;
+  const int b = mt / P.tiles_per_batch;
+  const int t0 = (mt - b * P.tiles_per_batch) * E - ACT_EPI_HALO;
+  tc_window_dma<I0, I1, N>((uintptr_t)(P.a + (int64_t)b * P.T * P.Cp), batch_bytes, dst, off,
+                   (uint32_t)((t0 - P.pad) * P.Cp * 2));
+}
+
+// weights bytes reserved for taps <= kmax: NSP rows x odd slots, rounded up to whole DMA instructions
+static constexpr int tc_wbytes(int C, int NS, int NPB, int kmax) {
+  const int nsp = (NS + 15) / 16 * 16;
+  const int kd = (kmax * C + 31) / 32 * 32;
+  const int slots = (kd / 8) % 2 ? kd / 8 : kd / 8 + 1;
+  return NPB * ((nsp * slots + 63) / 64) * 1024;
+}
+
 // C input channels, NS output channels per tile, NPB weight planes (1 = F16, 2 = F16W2), BM rows per tile,
-// R Activation1d rows per work item, WBYTES LDS bytes reserved for the weights (all planes)
-template <int C, int NS, int NPB, int BM, int R, int WBYTES, bool ACT, bool RES, bool OUTW, bool ACC>
-__global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
-  constexpr int NW = BM / 32, NT = NW * 64;
+// R Activation1d rows per work item, KMAX the largest tap count the LDS weight region is sized for.
+// NW = BM / 32 compute waves plus one loader wave (the last), which issues every window DMA and nothing else: vmcnt
+// is one in-order counter per wave, so with the window DMA issued by the compute waves after their epilogue stores
+// each window wait also waited for those stores to drain (scripts/microbench.py tphase, C48 k3 conv2: 12k of a
+// 25k-cycle tile); the loader's waits cover its own DMA only and the stores drain under the next tile's K loop.
+// Where the LDS holds the window apart from the staged tile (SEP: k <= 7 at C = 48), the loader DMAs the next tile's
+// window as soon as the K loop is done with the current one, under the epilogue.
+template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC>
+__global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P) {
+  constexpr int NW = BM / 32, NT = NW * 64;             // compute waves / threads
   constexpr int TM = 2, NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
   constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;  // window row: odd number of 16-B slots
   constexpr int RS = RSS * 16;
@@ -172,32 +215,40 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
   constexpr int OTS = NS + 4;                           // staged fp32 row stride (floats)
   constexpr int STAGE = BM * OTS * 4;
   constexpr int WINB = WIN_INSTR * 1024;
-  constexpr int REGION = STAGE > WINB ? STAGE : WINB;   // window, then (after the K loop) the staged tile
+  constexpr int WBYTES = tc_wbytes(C, NS, NPB, KMAX);
+  constexpr bool SEP = WBYTES + WINB + STAGE <= 163840;
+  constexpr int REGION = SEP ? WINB + STAGE : (STAGE > WINB ? STAGE : WINB);
   constexpr int SMEM = WBYTES + REGION;
   static_assert(SMEM <= 163840, "LDS");
+  static_assert(WIN_INSTR <= 60, "one wave's window DMA within the vmcnt range");
   static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
   static_assert(C % 8 == 0 && NS % 4 == 0, "geometry");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   char* const wl = smem;            // weights
-  char* const win = smem + WBYTES;  // window / staged tile
-  float* const ot = reinterpret_cast<float*>(win);
+  char* const win = smem + WBYTES;  // window (and, unless SEP, the staged tile after the K loop)
+  float* const ot = reinterpret_cast<float*>(SEP ? win + WINB : win);
+  // the window as an LDS-address-space pointer, cast once outside the loader's branch (a generic -> LDS cast inside it
+  // trips the gfx950 backend: "Operand has incorrect register class" on src_shared_base)
+  typedef __attribute__((address_space(3))) char lds_char_t;
+  lds_char_t* const win3 = (lds_char_t*)win;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = P.ksize, dil = P.dil;
   const int WS = P.wslots * 16;
   const int nslice = P.kd / 32;
+  const int cg = blockIdx.x % P.ncg;  // column group of this workgroup's tiles (ncg divides the grid stride)
+  const int n0 = cg * NS;
+  const int E = BM - 2 * ACT_EPI_HALO;  // emitted rows per tile
 
-  // ---- weights, once per workgroup: slot g of plane p -> row n = g / wslots, 16-B piece q = g % wslots
+  // ---- weights, once per workgroup (every wave): slot g of plane p -> row n = g / wslots, 16-B piece q = g % wslots
   {
     const int total = NSP * P.wslots;
     const int instr = (total + 63) / 64;
     for (int p = 0; p < NPB; ++p) {
-      for (int i = wave; i < instr; i += NW) {
+      for (int i = wave; i < instr; i += NW + 1) {
         const int g = i * 64 + lane;
         const int n = g / P.wslots, q = g - n * P.wslots;
         const bool ok = g < total && n < NS && q < P.kd / 8;
-        // column group of this workgroup's tiles is fixed: tiles are dealt so that ncg divides the stride
-        const int cg = blockIdx.x % P.ncg;
         const u16* src = ok ? P.w + p * P.w_lo + (int64_t)(cg * NS + n) * P.kd + q * 8
                             : reinterpret_cast<const u16*>(g_tconv_zero);
         tc_glds16(src, wl + p * (WBYTES / NPB) + i * 1024);
@@ -205,13 +256,52 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
     }
   }
 
+  if (wave == NW) {
+    // ---- loader: the window of each tile (rows [t0 - pad, t0 - pad + WR), slot g -> row g / RSS, piece g % RSS,
+    // pieces >= C / 8 zero), one barrier for each of the compute waves' per tile
+    // per-lane byte offsets of the window slots relative to row t0 - pad of the batch (tile-invariant); slots past
+    // the window or in a row's padding piece get an offset past any batch, which the buffer range check turns into
+    // zeros without a memory access (as are rows before 0 or past T: negative or too-large offsets)
+    const int WR = BM + (K - 1) * dil;
+    uint32_t off[WIN_INSTR];
+#pragma unroll
+    for (int i = 0; i < WIN_INSTR; ++i) {
+      const int g = i * 64 + lane;
+      const int r = g / RSS, q = g - r * RSS;
+      off[i] = (r < WR && q < C / 8) ? (uint32_t)((r * P.Cp + q * 8) * 2) : 0x7fffffffu;
+    }
+    const uint32_t batch_bytes = (uint32_t)P.T * (uint32_t)P.Cp * 2u;
+    int tile = blockIdx.x;
+    if (tile < P.ntiles) tc_window_tile<0, WIN_INSTR>(P, tile, E, batch_bytes, win3, off);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weights + the first window
+    // SEP: the next window's DMA issue (~100 cycles a piece) spread over the epilogue's barrier intervals, so that no
+    // compute-wave barrier waits for the whole issue (in one piece it held the staging barrier ~3.5k cycles)
+    constexpr bool RB = (RES || OUTW || ACC) && ACT;
+    constexpr int D1 = WIN_INSTR / 5, D2 = RB ? D1 + WIN_INSTR / 4 : D1;
+    for (; tile < P.ntiles; tile += gridDim.x) {
+      const int next = tile + gridDim.x;
+      const bool more = next < P.ntiles;
+      __syncthreads();  // A: the window of `tile` has landed
+      __syncthreads();  // B: the compute waves are done reading it
+      if (SEP && more) tc_window_tile<0, D1>(P, next, E, batch_bytes, win3, off);
+      __syncthreads();  // staged tile written
+      if constexpr (RB) {
+        if (SEP && more) tc_window_tile<D1, D2>(P, next, E, batch_bytes, win3, off);
+        __syncthreads();  // residual / state pass done
+      }
+      if (SEP && more) tc_window_tile<D2, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
+      __syncthreads();  // C: staged-tile reads retired
+      if (!SEP && more) tc_window_tile<0, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight DMA (the barrier A below publishes all)
+
   const int wr0 = wave * 32;  // first tile row of this wave
   const int q4 = lane >> 4, l16 = lane & 15;
   constexpr int NRES = (BM * (NS / 4) + NT - 1) / NT;  // residual float4 per thread
-  const int cg = blockIdx.x % P.ncg;
-  const int n0 = cg * NS;
-  const int E = BM - 2 * ACT_EPI_HALO;  // emitted rows per tile
-  float bias_r[TN];                     // this lane's output-column biases, loaded once
+  float bias_r[TN];                                     // this lane's output-column biases, loaded once
 #pragma unroll
   for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
 
@@ -222,9 +312,8 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
     const int b = mt / P.tiles_per_batch;
     const int e0 = (mt - b * P.tiles_per_batch) * E;  // first emitted row
     const int t0 = e0 - ACT_EPI_HALO;                 // first computed row
-    const int WR = BM + (K - 1) * dil;
 
-    // residual rows of the tile (clamped to [0, T)) into registers, ahead of the K loop
+    // residual rows of the tile (clamped to [0, T)) into registers, waited for in the epilogue
     float4 rv[NRES];
     if constexpr (RES) {
 #pragma unroll
@@ -235,17 +324,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
         rv[i] = *reinterpret_cast<const float4*>(P.res + ((int64_t)b * P.T + t) * P.N + n0 + (e < BM * (NS / 4) ? n : 0));
       }
     }
-    // input window rows [t0 - pad, t0 - pad + WR): slot g -> row g / RSS, piece g % RSS (pieces >= C/8 zero)
-    for (int i = wave; i < WIN_INSTR && !(P.ablate & 4); i += NW) {
-      const int g = i * 64 + lane;
-      const int r = g / RSS, q = g - r * RSS;
-      const int ts = t0 - P.pad + r;
-      const bool ok = r < WR && q < C / 8 && ts >= 0 && ts < P.T;
-      const u16* src = ok ? P.a + ((int64_t)b * P.T + ts) * P.Cp + q * 8 : reinterpret_cast<const u16*>(g_tconv_zero);
-      tc_glds16(src, win + i * 1024);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    __syncthreads();  // A
     tm.mark(0);
 
     // ---- barrier-free K loop over 32-deep slices of the dense K
@@ -293,7 +372,7 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
     }
     if (s < nslice) slice(s);
     tm.mark(1);
-    __syncthreads();  // every window read retired: the region becomes the staged tile
+    __syncthreads();  // B: every window read retired (the loader may refill it; unless SEP it becomes the staged tile)
     tm.mark(2);
     if (P.ablate & 1) {
       float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
@@ -302,11 +381,14 @@ __global__ __launch_bounds__(BM * 2, 1) void tconv_kernel(const TConvDev P) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sum == 123.f && P.out) P.out[tid] = sum;
+      __syncthreads();  // the epilogue's barriers, kept in step with the loader
+      if constexpr ((RES || OUTW || ACC) && ACT) __syncthreads();
+      __syncthreads();
       continue;
     }
 
     tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
-    __syncthreads();  // staged-tile reads retired before the next window DMA overwrites the region
+    __syncthreads();  // C: staged-tile reads retired
     tm.mark(6);
     if (tm.on) tm.ph[7] += 1;
   }
@@ -498,14 +580,6 @@ struct TConvCfg {
   int C, NS, NPB, BM;
 };
 
-// weights bytes reserved per configuration (k <= 11): NSP rows x odd slots, rounded up to whole DMA instructions
-static constexpr int tc_wbytes(int C, int NS, int NPB) {
-  const int nsp = (NS + 15) / 16 * 16;
-  const int kd = (11 * C + 31) / 32 * 32;
-  const int slots = (kd / 8) % 2 ? kd / 8 : kd / 8 + 1;
-  return NPB * ((nsp * slots + 63) / 64) * 1024;
-}
-
 bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
   if (knobs().tconv == 0) return false;
   if (prec != PREC_F16 && prec != PREC_F16W2) return false;
@@ -514,17 +588,17 @@ bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
   return C == 48 || C == 24;
 }
 
-template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
+template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC>
 static void tc_launch(const TConvDev& P, int grid, hipStream_t s) {
-  constexpr int WB = tc_wbytes(C, NS, NPB);
-  hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, WB, ACT, RES, OUTW, ACC>), dim3(grid), dim3(BM * 2), 0, s, P);
+  hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
 }
 
-template <int C, int NS, int NPB, int BM, int R>
+template <int C, int NS, int NPB, int BM, int R, int KMAX = 11>
 static int tc_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
-  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, true, false, false, false>(P, grid, s);
-  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, true, true, true, false>(P, grid, s);
-  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, false, true, false, true>(P, grid, s);
+  if (P.kd > (KMAX * C + 31) / 32 * 32) return set_error(ALCM_E_INVALID, "tconv: weights exceed the LDS reservation");
+  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, false, false, false>(P, grid, s);
+  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, true, true, false>(P, grid, s);
+  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, KMAX, false, true, false, true>(P, grid, s);
   else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
   return 0;
 }
@@ -615,7 +689,10 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     grid = std::max(P.ncg, grid / P.ncg * P.ncg);
     if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);
     else if (C == 48) {
-      if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+      // LDS weight region sized by the taps: k <= 7 leaves room for the window apart from the staged tile
+      if (npb == 2 && a.ksize <= 3) rc = tc_mode<48, 48, 2, 256, 12, 3>(P, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2 && a.ksize <= 7) rc = tc_mode<48, 48, 2, 256, 12, 7>(P, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
       else rc = tc_mode<48, 48, 1, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
     } else {
       if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);

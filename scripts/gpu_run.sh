@@ -27,7 +27,7 @@ for round in 1 2; do
   for v in $variants; do
     envs=""
     [ "$v" != "-" ] && envs=$(echo "$v" | tr ',' ' ')
-    name=$(echo "$v" | tr ',=' '_-')
+    name=$(echo "$v" | tr ',=/' '_-_')
     env $envs ALCM_BENCH_ALL_KERNELS=1 timeout -k 10 300 python -u bench.py $ARGS \
       > $out/ab_${round}_$name.json 2> $out/ab_${round}_$name.err || exit $?
     echo "$v: $(python -c "import json;d=json.load(open('$out/ab_${round}_$name.json'));print(d['value'], d['ms_per_step'])")" >> $out/ab.txt
