@@ -63,16 +63,20 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
 // halves the weight bytes (and doubles the window bytes, amortised over k taps).
 constexpr int W2_HALO = 64;  // max (k - 1) * dil
 
+// BM = 160 (waves 2 x 2 of 80 x 96, TM = 5): sequences of T = 312 rows as two tiles (320 rows) instead of three of 128
+// (384 rows, 768 tiles on the 512 workgroup slots of the chip: the VAE's k3 convs)
 template <int PREC, bool GEGLU, int BM = 128, int BN = 192>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
-  constexpr int TM = 4, TN = 6;
-  constexpr int WGM = BM / 64, WGN = 4 / WGM;   // wave grid
-  static_assert(WGM * WGN == 4 && WGN * TN * 16 == BN, "4 waves of 64 x 96");
+  constexpr int WGM = BM == 256 ? 4 : 2, WGN = 4 / WGM;  // wave grid
+  constexpr int TM = BM / WGM / 16, TN = 6;
+  constexpr int WR_ROWS = TM * 16;                        // rows per wave
+  static_assert(WGM * WGN == 4 && WGN * TN * 16 == BN && WGM * WR_ROWS == BM, "4 waves of (16 TM) x 96");
   constexpr int WROWS = BM + W2_HALO;
   constexpr int WBUF = WROWS * 128;      // window image
   constexpr int BBUF = BN * 128;         // weight image
-  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB (128 x 192) / 64 KB (256 x 96)
-  constexpr int WPW = WROWS / 8 / 4;     // window DMA instructions per wave (6 / 10)
+  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB (128 x 192) / 64 KB (256 x 96) / 76 KB (160 x 192)
+  constexpr int WPW = WROWS / 8 / 4;     // window DMA instructions per wave (6 / 10 / 7)
+  static_assert(WROWS % 32 == 0, "whole window DMA instructions per wave");
   constexpr int BPW = BN / 8 / 4;        // weight DMA instructions per wave per step (6 / 3)
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       for (int j = 0; j < BPW; ++j) glds16(bsrc[j] + off, smem + WBUF + buf * BBUF + (wave + 4 * j) * 1024);
     };
 
-    const int arow0 = wm * 64 + (lane & 15);
+    const int arow0 = wm * WR_ROWS + (lane & 15);
     const int nrow0 = wn * 96 + (lane & 15);
     const int bsw = lane & 7;
 
@@ -218,12 +222,14 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
     }
   }
 
-  // epilogue: one 64-row slice of the tile at a time through LDS (the K loop's last barrier retired every
-  // fragment read and DMA), whole row segments (768 / 384 B) with 16-B loads / stores
+  // epilogue: one wave row's slice of the tile (64 or 80 rows) at a time through LDS (the K loop's last barrier retired
+  // every fragment read and DMA), whole row segments (768 / 384 B) with 16-B loads / stores
   constexpr int OTS = BN + 4;
+  static_assert(WR_ROWS * OTS * 4 <= SMEM, "staged slice");
   float* ot = reinterpret_cast<float*>(smem);
   constexpr int cq = BN / 4;
-  constexpr int PER = 64 * cq / 256;  // float4 per thread per slice (12 / 6)
+  constexpr int PER = WR_ROWS * cq / 256;  // float4 per thread per slice (12 / 6 / 15)
+  static_assert(WR_ROWS * cq % 256 == 0, "whole float4 passes");
   // GEGLU: this thread's bias columns (the same in every slice), loaded once up front: loaded next to each store they
   // made every store-load pair a vmcnt(0) round trip (24 serialised per tile)
   float4 gbv[GEGLU ? PER : 1];
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
             ot[(i * 16 + (lane >> 4) * 4 + r) * OTS + wn * 96 + j * 16 + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
-    const int r0 = t0 + h * 64;
+    const int r0 = t0 + h * WR_ROWS;
     if constexpr (GEGLU) {
       const int No = P.N / 2;
       for (int e = 0; e < PER; ++e) {
@@ -262,7 +268,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       }
     } else {
       // passes of PH loads (residual, accumulate, bias): the other halves' accumulators are still live in half 0
-      constexpr int PH = BN == 192 ? PER / 4 : PER / 2;
+      constexpr int PH = PER % 4 == 0 ? (BN == 192 ? PER / 4 : PER / 2) : PER / 5;
+      static_assert(PER % PH == 0, "load passes");
 #pragma unroll
       for (int e0 = 0; e0 < PER; e0 += PH) {
       float4 rv[PH], pv[PH], bv[PH];  // (bias with them: loaded next to each store it cost a vmcnt(0) per store)
@@ -730,7 +737,17 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   if (a.geglu_plane && (a.res || a.accumulate || (((uintptr_t)a.geglu_plane) & 3))) return 0;
   // wconv2 tile: 256 x 96 halves the weight bytes every tile fetches (see the kernel comment)
   const bool t256 = !ragged && wconv2_tile256(a);
-  const int BM2 = t256 ? 256 : 128, BN2 = t256 ? 96 : 192;
+  // 160-row tiles where rounds x tile rows over the two-workgroup slots of the chip drop: the VAE's T = 312 k3 convs at
+  // N = 1536 (768 tiles of 128 rows = 1.5 rounds, 512 of 160 = one; 1.82 -> 1.43 ms/step); N = 768
+  // (384 tiles, one round either way) stays at 128
+  bool t160 = false;
+  if (!t256 && !a.geglu_plane && !strided && a.N % 192 == 0) {
+    const int64_t slots = 2 * (int64_t)g_ncu, tn = a.N / 192;
+    const int64_t r128 = ((int64_t)a.B * ((a.T + 127) / 128) * tn + slots - 1) / slots;
+    const int64_t r160 = ((int64_t)a.B * ((a.T + 159) / 160) * tn + slots - 1) / slots;
+    t160 = r160 * 160 < r128 * 128;
+  }
+  const int BM2 = t256 ? 256 : (t160 ? 160 : 128), BN2 = t256 ? 96 : 192;
   if (a.N % BN2 == 0 || ragged) {
     WConvDev P{};
     P.a = (const u16*)a.a;
@@ -770,6 +787,8 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     };
     if (t256) {
       go(std::integral_constant<int, 256>{});
+    } else if (t160) {
+      go(std::integral_constant<int, 160>{});
     } else {
       go(std::integral_constant<int, 128>{});
     }

@@ -359,6 +359,30 @@ def test_opconv_wide(K, C, T, k, dil, prec, monkeypatch):
         assert rel_l2(y.numpy(), y0.numpy()) < 1e-5, (knob, var)
 
 
+@pytest.mark.parametrize("prec", [0, 2])
+def test_wconv2_tile160(K, prec, monkeypatch):
+    """160-row wconv2 tiles (chosen where they take fewer rounds of the chip's workgroup slots: T = 312 as two tiles
+    instead of three, 24 x 2 x 8 = 384 tiles instead of 576): vs F.conv1d (fp32, on the GPU) and vs the 128-row
+    opconv_kernel on the same operand planes (ALCM_WCONV=0)."""
+    B, T, C, N, k = 24, 312, 256, 1536, 3
+    x = _r((B, T, C), 90)
+    w, bias = _r((N, C, k), 91, 0.7 / np.sqrt(C * k)), _r((N,), 92, 0.05)
+    r = _r((B, T, N), 93)
+    ref = (F.conv1d(dev(x).permute(0, 2, 1), dev(w), dev(bias), padding=1).permute(0, 2, 1) + dev(r)).cpu()
+    pl = K.operand_planes(dev(x), prec)
+    y = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    assert rel_l2(y.numpy(), ref.numpy()) < TOL[prec]
+    from audiolcm_amd import _hip
+    monkeypatch.setenv("ALCM_WCONV", "0")
+    _hip.reload_knobs()
+    try:
+        y0 = K.opconv(pl, C, dev(w), dev(bias), 1, prec, residual=dev(r)).cpu()
+    finally:
+        monkeypatch.delenv("ALCM_WCONV")
+        _hip.reload_knobs()
+    assert rel_l2(y.numpy(), y0.numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("C,N,T,k,act", [(256, 200, 700, 1, 2), (256, 200, 700, 3, 0), (768, 1000, 300, 1, 2),
                                           (192, 388, 1300, 3, 1)])
 @pytest.mark.parametrize("prec", [0, 2])
