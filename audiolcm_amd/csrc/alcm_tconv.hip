@@ -400,8 +400,9 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
 // share a CU: the Activation1d epilogue (VALU) of one overlaps the K loop (MFMA) of the other, which the
 // resident-weight kernel (one workgroup per CU at C >= 48) cannot do.  Ring slot layout: row n of 64 B (32 fp16 of
 // K), its 16-B piece q at physical piece q ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows).
-template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC>
-__global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
+// OCC workgroups per CU: 2, or 4 (<= 128 VGPRs: the residual is then loaded in the epilogue, not prefetched)
+template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   constexpr int PD = 2;  // weight slices in flight ahead of the one consumed (3: equal, the K loop is LDS-read bound)
   constexpr int NT = 256, RPW = BM / 4, TM = RPW / 16;
   constexpr int NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void tconv2_kernel(const TConvDev P) {
   constexpr int NRES = (BM * (NS / 4) + NT - 1) / NT;
   // residual prefetched into registers at the tile start (C = 96: loaded in the epilogue; prefetched, its 72 registers
   // beside the accumulators spill and the window wait covers it: 0.59 -> 0.75 ms)
-  constexpr bool PRE = NRES <= 12;
+  constexpr bool PRE = NRES <= 12 && OCC == 2;
   float4 rv[PRE ? NRES : 1];
   if constexpr (RES && PRE) {
 #pragma unroll
@@ -603,12 +604,12 @@ static int tc_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, b
   return 0;
 }
 
-template <int C, int NS, int NPB, int BM, int R>
+template <int C, int NS, int NPB, int BM, int R, int OCC = 2>
 static int tc2_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
   const dim3 g(grid), blk(256);
-  if (act && !res && !outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, false, false, false>), g, blk, 0, s, P);
-  else if (act && res && outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, true, true, false>), g, blk, 0, s, P);
-  else if (!act && res && acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, false, true, false, true>), g, blk, 0, s, P);
+  if (act && !res && !outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, false, false, false, OCC>), g, blk, 0, s, P);
+  else if (act && res && outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, true, true, false, OCC>), g, blk, 0, s, P);
+  else if (!act && res && acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, false, true, false, true, OCC>), g, blk, 0, s, P);
   else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
   return 0;
 }
@@ -676,8 +677,11 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
       if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
       else rc = tc2_mode<48, 48, 1, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
     } else {
-      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);
+      // four workgroups per CU (6-row Activation1d runs and the residual loaded in the epilogue keep it at 128 VGPRs):
+      // conv2 + residual + Activation1d 0.61 -> 0.51 ms (k3), 0.70 -> 0.55 (k11), conv1 k3 0.39 -> 0.37, end to end
+      // -0.5 ms/step (gpurun_out/r5aa)
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 6, 4>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 256, 6, 4>(P, grid2, act, a.res, outw, acc_mode, s);
     }
   } else {
     // persistent: a multiple of ncg workgroups so a workgroup's column group (blockIdx % ncg) is the same for every
