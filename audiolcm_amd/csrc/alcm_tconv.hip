@@ -414,14 +414,14 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   constexpr int SLOT = NSP * 64 * NPB;                  // one K slice of every weight plane
   constexpr int SPI = (NSP * 4 * NPB + 63) / 64;        // DMA instructions per slice
   constexpr int DPW = (SPI + 3) / 4;                    // per wave (uniform: extra lanes write the scratch line)
-  constexpr int RING = 4;
+  constexpr int RING = OCC >= 3 ? 3 : 4;  // (3: slices two ahead still land in a slot whose reads retired)
   constexpr int WINB = WPW * 4 * 1024;
   constexpr int RINGB = RING * SLOT;
   constexpr int OTS = NS + 4;
   constexpr int STAGE = BM * OTS * 4;
   constexpr int REGION = (STAGE > WINB + RINGB ? STAGE : WINB + RINGB);
   constexpr int SMEM = REGION + 1024 * 4;               // + one scratch KB per wave for padding DMA instructions
-  static_assert(SMEM <= 81920, "two workgroups per CU");
+  static_assert(SMEM <= 163840 / OCC, "OCC workgroups per CU");
   static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
   static_assert(C % 8 == 0 && NS % 4 == 0 && RPW % 16 == 0, "geometry");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
