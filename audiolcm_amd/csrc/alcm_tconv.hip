@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   constexpr int SLOT = NSP * 64 * NPB;                  // one K slice of every weight plane
   constexpr int SPI = (NSP * 4 * NPB + 63) / 64;        // DMA instructions per slice
   constexpr int DPW = (SPI + 3) / 4;                    // per wave (uniform: extra lanes write the scratch line)
-  constexpr int RING = OCC >= 3 ? 3 : 4;  // (3: slices two ahead still land in a slot whose reads retired)
+  constexpr int RING = 4;
   constexpr int WINB = WPW * 4 * 1024;
   constexpr int RINGB = RING * SLOT;
   constexpr int OTS = NS + 4;
@@ -681,7 +681,8 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
       // conv2 + residual + Activation1d 0.61 -> 0.51 ms (k3), 0.70 -> 0.55 (k11), conv1 k3 0.39 -> 0.37, end to end
       // -0.5 ms/step (gpurun_out/r5aa)
       if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 6, 4>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 256, 6, 4>(P, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);  // (other policies; a W1 twin of
+      // the W2 instantiation's template arguments above made the compiler spill 84 B in the W2 kernel, 12 without)
     }
   } else {
     // persistent: a multiple of ncg workgroups so a workgroup's column group (blockIdx % ncg) is the same for every
