@@ -679,7 +679,11 @@ def test_activation1d_op(K, C, T, prec):
 
 @pytest.mark.parametrize("C,T,k,dil,prec", [(24, 1000, 11, 5, 3), (48, 700, 7, 3, 3), (96, 500, 3, 1, 2),
                                             (96, 333, 11, 5, 2), (24, 250, 3, 1, 2), (48, 2000, 11, 5, 2),
-                                            (48, 37, 3, 1, 3)])
+                                            (48, 37, 3, 1, 3),
+                                            # > 256 tiles: persistent workgroups walk several, the loader wave
+                                            # prefetching the next tile's window (k <= 7) or refilling after the
+                                            # epilogue (k = 11); C = 24 at four workgroups per CU
+                                            (48, 70000, 3, 1, 3), (48, 70000, 11, 5, 3), (24, 70000, 3, 1, 3)])
 @pytest.mark.parametrize("mode", ["conv1", "conv2", "last"])
 def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
     """alcm_opconv_dense (BigVGAN stages 3-5: dense K = tap*C + c, weights resident in LDS, persistent tiles) == the
