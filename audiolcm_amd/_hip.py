@@ -95,6 +95,7 @@ _SIGS = [
     ("alcm_model_set_precision", C.c_int, [vp, C.c_int]),
     ("alcm_model_set_resblock_streams", C.c_int, [vp, C.c_int]),
     ("alcm_reload_knobs", C.c_int, []),
+    ("alcm_debug_tconv_trace", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     ("alcm_dit_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_dit_embed_context", C.c_int, [vp, fp, C.c_int, fp, vp, C.c_size_t, vp]),
     ("alcm_dit_forward", C.c_int, [vp, fp, vp, fp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
@@ -169,6 +170,14 @@ def ptr(t) -> Optional[int]:
 def reload_knobs() -> None:
     """Re-read the ALCM_* diagnostic switches (the library reads them once at load)."""
     check(lib().alcm_reload_knobs(), "alcm_reload_knobs")
+
+
+def debug_tconv_trace(reset: bool = True) -> list:
+    """Diagnostics: the tail-conv phase trace (ALCM_XP3=1) since the last reset — 7 phase cycle sums and the wave-tile
+    count (alcm_debug_tconv_trace)."""
+    out = (C.c_ulonglong * 8)()
+    check(lib().alcm_debug_tconv_trace(out, 1 if reset else 0), "alcm_debug_tconv_trace")
+    return list(out)
 
 
 PEAK_BF16_FLOPS = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)

@@ -332,11 +332,8 @@ def bench_tphase(B=32):
     """per-phase shader-clock breakdown of the tail convs as the model runs them (ALCM_XP3=1 trace): cycles per tile
     per wave of [window + first slices, K loop, post-loop barrier, stage v, residual + fp32 out, Activation1d, final
     barrier]; TCONFIGS = C:k:mode,... (mode conv1 / conv2)"""
-    import ctypes
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    L = _hip.lib()
-    out8 = (ctypes.c_ulonglong * 8)()
     os.environ["ALCM_XP3"] = "1"
     _hip.reload_knobs()
     cfgs = os.environ.get("TCONFIGS", "96:3:conv2,96:11:conv2,96:11:conv1,48:3:conv2,48:11:conv2,24:3:conv2,24:11:conv2")
@@ -357,10 +354,9 @@ def bench_tphase(B=32):
             os.environ[os.environ.get("XP_NAME", "ALCM_XP0")] = xv
             _hip.reload_knobs()
             run()
-            L.alcm_debug_tconv_trace(out8, 1)
+            _hip.debug_tconv_trace()
             ms = timeit(run, reps=5)
-            L.alcm_debug_tconv_trace(out8, 1)
-            v = list(out8)
+            v = _hip.debug_tconv_trace()
             tiles = max(v[7], 1)
             ph = " ".join(f"{x / tiles:7.0f}" for x in v[:7])
             print(f"tphase C={C:3d} k={k:2d} {mode} xp={xv}: {ms:6.3f} ms  cycles/tile/wave [win kloop bar stage res act "
