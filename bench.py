@@ -77,6 +77,68 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def visible_gpus(env=None) -> int:
+    """GPUs this process may use, counted WITHOUT creating a HIP context: the length of HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when one is set (the narrowest wins), else
+    torch.cuda.device_count() (which on this ROCm image enumerates devices without initialising one)."""
+    env = os.environ if env is None else env
+    counts = [len([d for d in env[k].split(",") if d.strip() != ""])
+              for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES") if k in env]
+    if counts:
+        return min(counts)
+    return torch.cuda.device_count()
+
+
+def launch_plan(gpus: int, device_map, env, n_visible: int):
+    """What `bench.py --gpus N` does before anything touches a GPU.
+
+    Returns None when this process is itself a rank (N = 1, or started by torch.distributed.run, which sets
+    WORLD_SIZE), else the rank count to spawn.  Raises ValueError on a mismatch: --gpus != WORLD_SIZE under
+    torchrun, --gpus < 1, a --device-map whose length is not N, or more GPUs (or a device-map index beyond those)
+    than are visible."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least one GPU")
+    dmap = [int(x) for x in device_map.split(",")] if device_map else None
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise ValueError(f"--gpus {gpus} but torch.distributed.run started WORLD_SIZE={world} ranks")
+        if dmap is not None and len(dmap) < world:
+            raise ValueError(f"--device-map {device_map} names {len(dmap)} GPUs for {world} ranks")
+        return None
+    if dmap is not None and len(dmap) != gpus:
+        raise ValueError(f"--device-map {device_map} names {len(dmap)} GPUs for --gpus {gpus}")
+    need = max(dmap) + 1 if dmap else gpus
+    if need > n_visible:
+        raise ValueError(f"--gpus {gpus}{' --device-map ' + device_map if dmap else ''} needs {need} GPUs, "
+                         f"{n_visible} visible")
+    return gpus if gpus > 1 else None
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, script: str = None) -> int:
+    """--gpus N > 1 without torch.distributed.run: start the N ranks (one process per GPU) as children of this
+    process through torch.distributed.run on 127.0.0.1, forwarding every flag.  This process never initialises a
+    GPU and never execs; it relays the children's stdout (rank 0's JSON line is the only JSON there) and returns
+    torch.distributed.run's exit status (non-zero when any rank failed)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", script or os.path.abspath(__file__)] + list(argv)
+    log(f"starting {n} ranks: {' '.join(cmd[1:])}")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 class Heartbeat:
     """Prints a progress line every `every` seconds while a long host-side phase runs."""
 
@@ -293,6 +355,14 @@ def components(a):
 
 def main():
     a = parse()
+    try:
+        spawn = launch_plan(a.gpus, a.device_map, os.environ,
+                            visible_gpus() if "WORLD_SIZE" not in os.environ else a.gpus)
+    except ValueError as e:
+        log(f"error: {e}")
+        sys.exit(2)
+    if spawn:
+        sys.exit(spawn_ranks(spawn, sys.argv[1:]))
     from audiolcm_amd import _hip, recipe
     from audiolcm_amd.distributed import all_gather_rows, all_reduce_max, barrier, init_from_env
     from audiolcm_amd.pipeline import AudioLCMPipeline
@@ -404,7 +474,8 @@ def main():
         if tr:  # HBM bytes per launch from the committed PMC passes of this kernel
             roofline["traffic"] = tr["bytes_per_launch"]
             roofline["traffic_source"] = tr["source"]
-    line = dict(metric=METRIC, value=round(value, 2), unit="audio-s/s", n_gpus=world, steps=a.steps,
+    line = dict(metric=METRIC, value=round(value, 2), unit="audio-s/s",
+                n_gpus=dist.get_world_size() if dist.is_initialized() else world, steps=a.steps,
                 warmup=a.warmup, ms_per_step=round(1e3 * dt / a.steps, 2), higher_is_better=True, scaling="weak",
                 vs_baseline=None,
                 dtype=DTYPES[a.mode],

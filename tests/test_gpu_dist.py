@@ -34,23 +34,43 @@ def _run(cmd, tmp_path, name):
     return json.loads(lines[0])
 
 
-def test_bench_world2_gathers_bit_identical_waveforms(tmp_path):
+@pytest.fixture(scope="module")
+def world1_64(tmp_path_factory):
+    """One process generating the 64 prompt ids (the reference for both world-2 forms below)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    tmp = tmp_path_factory.mktemp("w1")
+    one = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--batch", "64", "--dump-wav",
+                str(tmp / "w1.npy")] + ARGS, tmp, "world1")
+    assert one["config"]["global_batch"] == 64 and one["n_gpus"] == 1
+    w1 = np.load(tmp / "w1.npy")
+    assert w1.shape == (64, 159744) and np.isfinite(w1).all() and np.abs(w1).max() > 0
+    return w1
+
+
+def test_bench_world2_gathers_bit_identical_waveforms(tmp_path, world1_64):
     bench = os.path.join(REPO, "bench.py")
-    one = _run([sys.executable, bench, "--gpus", "1", "--batch", "64", "--dump-wav", str(tmp_path / "w1.npy")]
-               + ARGS, tmp_path, "world1")
     two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                 "--master-addr=127.0.0.1", "--master-port=29583", bench, "--gpus", "2", "--batch", "32",
                 "--dist-backend", "gloo", "--device-map", "0,0", "--dump-wav", str(tmp_path / "w2.npy")] + ARGS,
                tmp_path, "world2")
-    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 64 and one["config"]["global_batch"] == 64
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 64
     assert two["value"] > 0 and two["ms_per_step"] > 0
-    w1, w2 = np.load(tmp_path / "w1.npy"), np.load(tmp_path / "w2.npy")
-    assert w1.shape == w2.shape == (64, 159744)
-    assert np.isfinite(w1).all() and np.abs(w1).max() > 0
-    assert np.array_equal(w1, w2)
+    w2 = np.load(tmp_path / "w2.npy")
+    assert w2.shape == (64, 159744)
+    assert np.array_equal(world1_64, w2)
+
+
+def test_bench_spawns_ranks_itself(tmp_path, world1_64):
+    """`bench.py --gpus 2` WITHOUT torch.distributed.run (the driver's N = 1 command form with N = 2): the parent
+    starts the two ranks itself (bench.spawn_ranks) and relays rank 0's line; n_gpus is the process group's size."""
+    two = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--batch", "32", "--dist-backend",
+                "gloo", "--device-map", "0,0", "--dump-wav", str(tmp_path / "ws.npy")] + ARGS, tmp_path, "spawn")
+    log = open(tmp_path / "spawn.log").read()
+    assert "starting 2 ranks" in log
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 64 and two["value"] > 0
+    assert np.array_equal(world1_64, np.load(tmp_path / "ws.npy"))
 
 
 def test_bench_rccl_world1_collectives(tmp_path):

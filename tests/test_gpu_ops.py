@@ -683,7 +683,8 @@ def test_activation1d_op(K, C, T, prec):
                                             # > 256 tiles: persistent workgroups walk several, the loader wave
                                             # prefetching the next tile's window (k <= 7) or refilling after the
                                             # epilogue (k = 11); C = 24 at four workgroups per CU
-                                            (48, 70000, 3, 1, 3), (48, 70000, 11, 5, 3), (24, 70000, 3, 1, 3)])
+                                            (48, 70000, 3, 1, 3), (48, 70000, 7, 3, 3), (48, 70000, 11, 5, 3),
+                                            (24, 70000, 3, 1, 3)])
 @pytest.mark.parametrize("mode", ["conv1", "conv2", "last"])
 def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
     """alcm_opconv_dense (BigVGAN stages 3-5: dense K = tap*C + c, weights resident in LDS, persistent tiles) == the
@@ -719,6 +720,54 @@ def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_ref)
         K.opconv(pl, C, dw, dev(bias), dil, prec, residual=r, out_scale=1 / 3, accumulate_into=o_d, dense=True)
         assert rel_l2(o_d.cpu().numpy(), o_ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("C,k,dil,mode", [(48, 11, 5, "conv2"), (48, 7, 3, "conv2"), (48, 3, 1, "conv1"),
+                                          (24, 3, 1, "conv2"), (24, 11, 5, "conv1"), (96, 11, 5, "conv2"),
+                                          (48, 11, 5, "last")])
+def test_tail_conv_multitile_vs_oracle(K, C, k, dil, mode):
+    """The narrow AMPBlock convs (vocoder/bigvgan/models.py:72-81, stages 3-5) on > 256 tiles — persistent resident
+    workgroups walking several tiles with the loader wave's next-window prefetch (C = 48), four streamed workgroups
+    per CU (C = 24), the C = 96 persistent streamed grid — against the fp32 ORACLE, not another HIP kernel:
+    F.conv1d on the fp16 operand values the kernel reads (weights in fp32; F16W2 carries them as hi + lo fp16) +
+    bias (+ residual), then oracle Activation1d (alias_free_torch/act.py:23-27).  fp32 state within accumulation-order
+    rounding (rel-L2 2e-5); the Activation1d plane within its fp16 rounding (rel-L2 1e-3, measured ~3e-4)."""
+    from oracle import alcm_oracle as O
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    B, T = 2, 70000
+    prec = 2 if C == 96 else 3
+    x = _r((B, T, C), 160)
+    w, bias = _r((C, C, k), 161, 0.7 / np.sqrt(C * k)), _r((C,), 162, 0.05)
+    r = _r((B, T, C), 163)
+    a, bt = _r((C,), 164, 0.3), _r((C,), 165, 0.3)
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    pl = K.operand_planes(dev(x), prec)
+    w_k = w.half().float() if prec == 2 else w   # F16: fp16 weights; F16W2: hi + lo fp16 (~fp32)
+    ref = F.conv1d(x.half().float().permute(0, 2, 1), w_k, bias, padding=(k - 1) * dil // 2, dilation=dil)
+    if mode != "conv1":
+        ref = ref + r.permute(0, 2, 1)
+    act = (dev(a), dev(bt), f, f)
+    if mode == "conv1":
+        _, pl_d = K.opconv(pl, C, dev(w), dev(bias), dil, prec, act=act, fp32_out=False, dense=True)
+    elif mode == "conv2":
+        y_d, pl_d = K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), act=act, dense=True)
+        e_y = rel_l2(y_d.cpu().permute(0, 2, 1).numpy(), ref.numpy())
+        print(f"tail {mode} C{C} k{k}: state rel-L2 {e_y:.2e}")
+        assert e_y < 2e-5
+    else:
+        o0 = _r((B, T, C), 166)
+        o_d = dev(o0.clone())
+        K.opconv(pl, C, dev(w), dev(bias), dil, prec, residual=dev(r), out_scale=1 / 3, accumulate_into=o_d,
+                 dense=True)
+        e_o = rel_l2(o_d.cpu().numpy(), (o0 + ref.permute(0, 2, 1) / 3).numpy())
+        print(f"tail last C{C} k{k}: accumulated rel-L2 {e_o:.2e}")
+        assert e_o < 2e-5
+        return
+    ref_act = O.activation1d(ref, a, bt, f, f).permute(0, 2, 1)
+    got = pl_d[0, ..., :C].cpu().view(torch.float16).float()
+    e_a = rel_l2(got.numpy(), ref_act.numpy())
+    print(f"tail {mode} C{C} k{k}: Activation1d plane rel-L2 {e_a:.2e}")
+    assert torch.isfinite(got).all() and e_a < 1e-3
 
 
 @pytest.mark.parametrize("C,T", [(192, 37), (384, 300), (768, 2496), (192, 1000)])
