@@ -173,7 +173,7 @@ def reload_knobs() -> None:
 
 
 def debug_tconv_trace(reset: bool = True) -> list:
-    """Diagnostics: the tail-conv phase trace (ALCM_XP3=1) since the last reset — 7 phase cycle sums and the wave-tile
+    """Diagnostics: the tail-conv phase trace (ALCM_TCONV_TRACE=1; the first call allocates the buffer) since the last reset — 7 phase cycle sums and the wave-tile
     count (alcm_debug_tconv_trace)."""
     out = (C.c_ulonglong * 8)()
     check(lib().alcm_debug_tconv_trace(out, 1 if reset else 0), "alcm_debug_tconv_trace")

@@ -111,8 +111,11 @@ struct Knobs {
   int opconv_tile = 0;           // ALCM_OPCONV_TILE: narrow-layer tile variant
   bool serial_resblocks = false; // ALCM_SERIAL_RESBLOCKS: default of alcm_model_set_resblock_streams
   bool prof_shapes = false;      // ALCM_PROF_SHAPES: split profile rows per layer shape
-  int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of tconv_kernel (1 no epilogue,
-                                 // 2 no MFMA, 4 no window DMA)
+  int tconv_ablate = 0;          // ALCM_TCONV_ABLATE: timing-only ablation bits of the tail convs (1 no epilogue,
+                                 // 2 no MFMA, 4 no window DMA, 8 no plane stores, 16 no fp32 state stores); selects
+                                 // their diagnostics instantiation
+  bool tconv_trace = false;      // ALCM_TCONV_TRACE: per-phase shader-clock trace of the tail convs (alcm_debug_tconv_trace;
+                                 // diagnostics instantiation)
   int lin1 = -1;                 // ALCM_LIN1: single-plane 1x1 convs on lin_plane_kernel (1: 32-deep 4-stage ring, 2: 64-deep
                                  // double-buffered, -1: 64-deep for plane outputs), 0 = wconv2
   int tconv = 1;                 // ALCM_TCONV: narrow conv for BigVGAN stages 3-5: 1 by shape, 2 streamed weights,

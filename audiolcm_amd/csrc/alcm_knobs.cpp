@@ -27,6 +27,7 @@ static Knobs read_knobs() {
   k.tconv = env_int("ALCM_TCONV", 1);
   k.lin1 = env_int("ALCM_LIN1", -1);
   k.tconv_ablate = env_int("ALCM_TCONV_ABLATE", 0);
+  k.tconv_trace = env_int("ALCM_TCONV_TRACE", 0) != 0;
   k.act_mfma = env_int("ALCM_ACT_MFMA", 1);
   k.act_defer = env_int("ALCM_ACT_DEFER", 1);
   k.xp[0] = env_int("ALCM_XP0", 0);

@@ -48,14 +48,17 @@ struct TConvDev {
   ActEpiDev act;      // act.plane == null: no Activation1d
   int tiles_per_batch, ntiles, ncg;  // ncg: column groups (N / NS)
   int wslots;         // 16-B slots per LDS weight row (odd)
-  int ablate;         // diagnostics (ALCM_TCONV_ABLATE, timing only, results wrong): 1 no epilogue, 2 no MFMA,
-                      // 4 no window DMA, 8 no plane stores, 16 no fp32 state stores
-  int stagger;        // tconv2: s_sleep(127) count before the second half of a persistent grid starts
-  unsigned long long* trace;  // diagnostics (ALCM_XP3 = 1): per-phase shader-clock sums over waves and tiles, or null
+  // diagnostics, read only by the DG = true instantiations (chosen when ALCM_TCONV_ABLATE or ALCM_TCONV_TRACE is set;
+  // the production instantiations compile neither in):
+  int ablate;         // ALCM_TCONV_ABLATE (timing only, results wrong): 1 no epilogue, 2 no MFMA, 4 no window DMA,
+                      // 8 no plane stores, 16 no fp32 state stores
+  unsigned long long* trace;  // ALCM_TCONV_TRACE: per-phase shader-clock sums over waves and tiles, or null
 };
 
 // phase timer of the diagnostics trace: wave-uniform shader-clock stamps, summed per phase over the tiles of a wave
-// and added to P.trace by lane 0 at the end (vector atomics)
+// and added to P.trace by lane 0 at the end (vector atomics).  TcTimer<false> (the production instantiations) is
+// empty: no registers, no clock reads, no atomics
+template <bool DG>
 struct TcTimer {
   bool on;
   unsigned long long last, ph[8];
@@ -70,11 +73,21 @@ struct TcTimer {
     ph[i] += t - last;
     last = t;
   }
+  __device__ __forceinline__ void tile() {
+    if (on) ph[7] += 1;
+  }
   __device__ __forceinline__ void flush(unsigned long long* out) {
     if (!on || (threadIdx.x & 63)) return;
     unsigned long long* o = out + (blockIdx.x & 63) * 8;  // 64 slot sets: no single-address contention
     for (int i = 0; i < 8; ++i) atomicAdd(o + i, ph[i]);
   }
+};
+template <>
+struct TcTimer<false> {
+  __device__ __forceinline__ void init(bool) {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void tile() {}
+  __device__ __forceinline__ void flush(unsigned long long*) {}
 };
 
 __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
@@ -85,11 +98,11 @@ __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
 // stride NS + 4 floats; the caller's barrier retired every K-loop read of that region), + residual (rv: the tile
 // rows' residual, prefetched as float4 element e = tid + i * NT), fp32 state / accumulated output of the owned rows,
 // Activation1d of the owned rows into the next conv's planes
-template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, bool RES, bool OUTW, bool ACC,
+template <int NS, int BM, int R, int TM, int TN, int NT, int NRES, bool ACT, bool RES, bool OUTW, bool ACC, bool DG,
           bool PRE = true>
 __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const float (&bias_r)[TN],
                                           const float4 (&rv)[PRE ? NRES : 1], float* ot, int wr0, int t0, int e0, int E,
-                                          int b, int n0, const TConvDev& P, TcTimer& tm) {
+                                          int b, int n0, const TConvDev& P, TcTimer<DG>& tm) {
   constexpr int OTS = NS + 4;
   const int tid = threadIdx.x, lane = tid & 63, q4 = lane >> 4, l16 = lane & 15;
   // v = conv + bias -> LDS
@@ -137,7 +150,7 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
         v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
         if constexpr (ACT) *reinterpret_cast<float4*>(ot + m * OTS + n) = v;
       }
-      if ((OUTW || ACC) && t >= e0 && t < e_hi && !(P.ablate & 16)) {
+      if ((OUTW || ACC) && t >= e0 && t < e_hi && !(DG && (P.ablate & 16))) {
         float* op = P.out + ((int64_t)b * P.T + t) * P.N + n0 + n;
         if constexpr (ACC) {
           v.x *= P.out_scale; v.y *= P.out_scale; v.z *= P.out_scale; v.w *= P.out_scale;
@@ -153,7 +166,7 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
   }
   tm.mark(4);
   if constexpr (ACT) {
-    if (P.ablate & 8) act_epilogue_ct<PREC_F16, R, NS / 2, true>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
+    if (DG && (P.ablate & 8)) act_epilogue_ct<PREC_F16, R, NS / 2, true>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
     else act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, tid, NT);
   }
   tm.mark(5);
@@ -177,10 +190,10 @@ __device__ __forceinline__ void tc_window_dma(uintptr_t base, uint32_t bytes, __
 }
 
 // the loader's window DMA of one tile (rows [t0 - pad, t0 - pad + WR) of its batch), slots [I0, I1)
+// (the diagnostics' "no window DMA" bit is tested by the caller: a template flag here fails the host pass)
 template <int I0, int I1, int N>
 __device__ __forceinline__ void tc_window_tile(const TConvDev& P, int tile, int E, uint32_t batch_bytes,
                                                __attribute__((address_space(3))) char* dst, const uint32_t (&off)[N]) {
-  if (P.ablate & 4) return;
   const int mt = tile / P.ncg;
   const int b = mt / P.tiles_per_batch;
   const int t0 = (mt - b * P.tiles_per_batch) * E - ACT_EPI_HALO;
@@ -204,7 +217,8 @@ static constexpr int tc_wbytes(int C, int NS, int NPB, int kmax) {
 // 25k-cycle tile); the loader's waits cover its own DMA only and the stores drain under the next tile's K loop.
 // Where the LDS holds the window apart from the staged tile (SEP: k <= 7 at C = 48), the loader DMAs the next tile's
 // window as soon as the K loop is done with the current one, under the epilogue.
-template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC>
+// DG: the diagnostics instantiation (ablation bits, phase trace); false in production.
+template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC, bool DG>
 __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P) {
   constexpr int NW = BM / 32, NT = NW * 64;             // compute waves / threads
   constexpr int TM = 2, NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
@@ -271,8 +285,9 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
       off[i] = (r < WR && q < C / 8) ? (uint32_t)((r * P.Cp + q * 8) * 2) : 0x7fffffffu;
     }
     const uint32_t batch_bytes = (uint32_t)P.T * (uint32_t)P.Cp * 2u;
+    const bool dma = !(DG && (P.ablate & 4));
     int tile = blockIdx.x;
-    if (tile < P.ntiles) tc_window_tile<0, WIN_INSTR>(P, tile, E, batch_bytes, win3, off);
+    if (dma && tile < P.ntiles) tc_window_tile<0, WIN_INSTR>(P, tile, E, batch_bytes, win3, off);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weights + the first window
     // SEP: the next window's DMA issue (~100 cycles a piece) spread over the epilogue's barrier intervals, so that no
     // compute-wave barrier waits for the whole issue (in one piece it held the staging barrier ~3.5k cycles)
@@ -283,15 +298,15 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
       const bool more = next < P.ntiles;
       __syncthreads();  // A: the window of `tile` has landed
       __syncthreads();  // B: the compute waves are done reading it
-      if (SEP && more) tc_window_tile<0, D1>(P, next, E, batch_bytes, win3, off);
+      if (dma && SEP && more) tc_window_tile<0, D1>(P, next, E, batch_bytes, win3, off);
       __syncthreads();  // staged tile written
       if constexpr (RB) {
-        if (SEP && more) tc_window_tile<D1, D2>(P, next, E, batch_bytes, win3, off);
+        if (dma && SEP && more) tc_window_tile<D1, D2>(P, next, E, batch_bytes, win3, off);
         __syncthreads();  // residual / state pass done
       }
-      if (SEP && more) tc_window_tile<D2, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
+      if (dma && SEP && more) tc_window_tile<D2, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
       __syncthreads();  // C: staged-tile reads retired
-      if (!SEP && more) tc_window_tile<0, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
+      if (dma && !SEP && more) tc_window_tile<0, WIN_INSTR>(P, next, E, batch_bytes, win3, off);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     return;
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
 #pragma unroll
   for (int j = 0; j < TN; ++j) bias_r[j] = (P.bias && j * 16 + l16 < NS) ? P.bias[n0 + j * 16 + l16] : 0.f;
 
-  TcTimer tm;
+  TcTimer<DG> tm;
   tm.init(P.trace != nullptr);
   for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
     const int mt = tile / P.ncg;
@@ -349,7 +364,7 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
         bh[j] = *reinterpret_cast<const bf16x8*>(brow + j * 16 * WS + kk * 2);
         if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(brow + WBYTES / 2 + j * 16 * WS + kk * 2);
       }
-      if (P.ablate & 2) {
+      if (DG && (P.ablate & 2)) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
@@ -374,7 +389,7 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
     tm.mark(1);
     __syncthreads();  // B: every window read retired (the loader may refill it; unless SEP it becomes the staged tile)
     tm.mark(2);
-    if (P.ablate & 1) {
+    if (DG && (P.ablate & 1)) {
       float sum = 0.f;  // keep every accumulator (and so the whole K loop) live
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -387,10 +402,10 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
       continue;
     }
 
-    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
+    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, DG>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
     __syncthreads();  // C: staged-tile reads retired
     tm.mark(6);
-    if (tm.on) tm.ph[7] += 1;
+    tm.tile();
   }
   tm.flush(P.trace);
 }
@@ -400,8 +415,9 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
 // share a CU: the Activation1d epilogue (VALU) of one overlaps the K loop (MFMA) of the other, which the
 // resident-weight kernel (one workgroup per CU at C >= 48) cannot do.  Ring slot layout: row n of 64 B (32 fp16 of
 // K), its 16-B piece q at physical piece q ^ ((n >> 2) & 3) (conflict-free ds_read_b128 of 16 consecutive rows).
-// OCC workgroups per CU: 2, or 4 (<= 128 VGPRs: the residual is then loaded in the epilogue, not prefetched)
-template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC, int OCC = 2>
+// OCC workgroups per CU: 2, or 4 (<= 128 VGPRs: the residual is then loaded in the epilogue, not prefetched).
+// STG: s_sleep(127) count before the second half of a persistent grid starts (C = 96); DG as tconv_kernel.
+template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC, int OCC, int STG, bool DG>
 __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   constexpr int PD = 2;  // weight slices in flight ahead of the one consumed (3: equal, the K loop is LDS-read bound)
   constexpr int NT = 256, RPW = BM / 4, TM = RPW / 16;
@@ -436,11 +452,12 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   const int nslice = P.kd / 32;
   const int E = BM - 2 * ACT_EPI_HALO;
   // persistent grid (C = 96): the second half of the workgroups (the second workgroup of each CU)
-  // starts P.stagger sleeps late, so the two workgroups of a CU alternate K loop (MFMA) and Activation1d epilogue
+  // starts STG sleeps late, so the two workgroups of a CU alternate K loop (MFMA) and Activation1d epilogue
   // (VALU) instead of running both phases in lockstep
-  if (P.stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
-    for (int i = 0; i < P.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  TcTimer tm;
+  if constexpr (STG > 0)
+    if ((int)blockIdx.x >= (int)gridDim.x / 2)
+      for (int i = 0; i < STG; ++i) __builtin_amdgcn_s_sleep(127);
+  TcTimer<DG> tm;
   tm.init(P.trace != nullptr);
   for (int tile = blockIdx.x; tile < P.ntiles; tile += gridDim.x) {
   const int mt = tile / P.ncg, cg = tile - mt * P.ncg;
@@ -535,7 +552,7 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dil) * RS + c * 2);
-    if (P.ablate & 2) {
+    if (DG && (P.ablate & 2)) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
@@ -557,7 +574,7 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
   }
   tm.mark(1);
   tm.mark(2);
-  if (P.ablate & 1) {
+  if (DG && (P.ablate & 1)) {
     float sum = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -566,16 +583,18 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
     if (sum == 123.f && P.out) P.out[tid] = sum;
     continue;
   }
-  tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
+  tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, DG, PRE>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P,
+                                                                      tm);
   __syncthreads();  // staged-tile reads retired before the next tile's DMA overwrites the region
   tm.mark(6);
-  if (tm.on) tm.ph[7] += 1;
+  tm.tile();
   }
   tm.flush(P.trace);
 }
 
 // -------------------------------------------------------------------------------------------------- host
-unsigned long long* g_tc_trace = nullptr;  // diagnostics trace buffer (8 sums), allocated on first use
+unsigned long long* g_tc_trace = nullptr;  // diagnostics trace buffer (64 x 8 sums), allocated by the first
+                                           // alcm_debug_tconv_trace call (never inside a launch path)
 
 struct TConvCfg {
   int C, NS, NPB, BM;
@@ -590,26 +609,32 @@ bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
 }
 
 template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC>
-static void tc_launch(const TConvDev& P, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
+static void tc_launch(const TConvDev& P, bool diag, int grid, hipStream_t s) {
+  if (diag) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC, true>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
+  else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC, false>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
 }
 
 template <int C, int NS, int NPB, int BM, int R, int KMAX = 11>
-static int tc_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
+static int tc_mode(const TConvDev& P, bool diag, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
   if (P.kd > (KMAX * C + 31) / 32 * 32) return set_error(ALCM_E_INVALID, "tconv: weights exceed the LDS reservation");
-  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, false, false, false>(P, grid, s);
-  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, true, true, false>(P, grid, s);
-  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, KMAX, false, true, false, true>(P, grid, s);
+  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, false, false, false>(P, diag, grid, s);
+  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, true, true, false>(P, diag, grid, s);
+  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, KMAX, false, true, false, true>(P, diag, grid, s);
   else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
   return 0;
 }
 
-template <int C, int NS, int NPB, int BM, int R, int OCC = 2>
-static int tc2_mode(const TConvDev& P, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
-  const dim3 g(grid), blk(256);
-  if (act && !res && !outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, false, false, false, OCC>), g, blk, 0, s, P);
-  else if (act && res && outw && !acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, true, true, true, false, OCC>), g, blk, 0, s, P);
-  else if (!act && res && acc) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, false, true, false, true, OCC>), g, blk, 0, s, P);
+template <int C, int NS, int NPB, int BM, int R, bool ACT, bool RES, bool OUTW, bool ACC, int OCC, int STG>
+static void tc2_launch(const TConvDev& P, bool diag, int grid, hipStream_t s) {
+  if (diag) hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, ACT, RES, OUTW, ACC, OCC, STG, true>), dim3(grid), dim3(256), 0, s, P);
+  else hipLaunchKernelGGL((tconv2_kernel<C, NS, NPB, BM, R, ACT, RES, OUTW, ACC, OCC, STG, false>), dim3(grid), dim3(256), 0, s, P);
+}
+
+template <int C, int NS, int NPB, int BM, int R, int OCC = 2, int STG = 0>
+static int tc2_mode(const TConvDev& P, bool diag, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
+  if (act && !res && !outw && !acc) tc2_launch<C, NS, NPB, BM, R, true, false, false, false, OCC, STG>(P, diag, grid, s);
+  else if (act && res && outw && !acc) tc2_launch<C, NS, NPB, BM, R, true, true, true, false, OCC, STG>(P, diag, grid, s);
+  else if (!act && res && acc) tc2_launch<C, NS, NPB, BM, R, false, true, false, true, OCC, STG>(P, diag, grid, s);
   else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
   return 0;
 }
@@ -634,14 +659,11 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   P.w = wd; P.w_lo = wd_lo; P.kd = kd; P.N = a.N;
   P.bias = a.bias; P.res = a.res; P.out = a.out; P.out_scale = a.out_scale; P.accumulate = a.accumulate;
   if (act) P.act = *act;
+  // the diagnostics instantiation only when a diagnostic is asked for (the trace needs its buffer, allocated by the
+  // first alcm_debug_tconv_trace call)
   P.ablate = knobs().tconv_ablate;
-  if (knobs().xp[3] == 1) {
-    if (!g_tc_trace) {
-      ALCM_HIP(hipMalloc(&g_tc_trace, 512 * sizeof(unsigned long long)));
-      ALCM_HIP(hipMemset(g_tc_trace, 0, 512 * sizeof(unsigned long long)));
-    }
-    P.trace = g_tc_trace;
-  }
+  if (knobs().tconv_trace) P.trace = g_tc_trace;
+  const bool diag = P.ablate != 0 || P.trace != nullptr;
   const int slots = kd / 8;
   P.wslots = slots % 2 ? slots : slots + 1;
   const int npb = a.prec == PREC_F16W2 ? 2 : 1;
@@ -665,23 +687,21 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     // box: k11 0.547 -> 0.491 ms, k3 0.300 -> 0.301, conv2 + residual 0.732 -> 0.695); C = 24 one workgroup per tile
     // (persistent measured +5..+17 %)
     int grid2 = (int)nt;
-    const int stg = C == 96 ? 3 : 0;
-    if (stg > 0) {
+    if (C == 96) {
       int dev = 0, ncu = 256;
       if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       grid2 = (int)std::min<int64_t>(nt, (int64_t)ncu * 2);
-      P.stagger = stg - 1;
     }
-    if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11>(P, grid2, act, a.res, outw, acc_mode, s);
+    if (C == 96) rc = tc2_mode<96, 96, 1, 192, 11, 2, 2>(P, diag, grid2, act, a.res, outw, acc_mode, s);
     else if (C == 48) {
-      if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<48, 48, 1, 256, 24>(P, grid2, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc2_mode<48, 48, 2, 256, 24>(P, diag, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<48, 48, 1, 256, 24>(P, diag, grid2, act, a.res, outw, acc_mode, s);
     } else {
       // four workgroups per CU (6-row Activation1d runs and the residual loaded in the epilogue keep it at 128 VGPRs):
       // conv2 + residual + Activation1d 0.61 -> 0.51 ms (k3), 0.70 -> 0.55 (k11), conv1 k3 0.39 -> 0.37, end to end
       // -0.5 ms/step (gpurun_out/r5aa)
-      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 6, 4>(P, grid2, act, a.res, outw, acc_mode, s);
-      else rc = tc2_mode<24, 24, 1, 256, 12>(P, grid2, act, a.res, outw, acc_mode, s);  // (other policies; a W1 twin of
+      if (npb == 2) rc = tc2_mode<24, 24, 2, 256, 6, 4>(P, diag, grid2, act, a.res, outw, acc_mode, s);
+      else rc = tc2_mode<24, 24, 1, 256, 12>(P, diag, grid2, act, a.res, outw, acc_mode, s);  // (other policies; a W1 twin of
       // the W2 instantiation's template arguments above made the compiler spill 84 B in the W2 kernel, 12 without)
     }
   } else {
@@ -692,16 +712,16 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     const int wgs = C == 24 ? 2 : 1;
     int grid = std::min<int64_t>(nt, (int64_t)ncu * wgs);
     grid = std::max(P.ncg, grid / P.ncg * P.ncg);
-    if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, grid, act, a.res, outw, acc_mode, s);
+    if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, diag, grid, act, a.res, outw, acc_mode, s);
     else if (C == 48) {
       // LDS weight region sized by the taps: k <= 7 leaves room for the window apart from the staged tile
-      if (npb == 2 && a.ksize <= 3) rc = tc_mode<48, 48, 2, 256, 12, 3>(P, grid, act, a.res, outw, acc_mode, s);
-      else if (npb == 2 && a.ksize <= 7) rc = tc_mode<48, 48, 2, 256, 12, 7>(P, grid, act, a.res, outw, acc_mode, s);
-      else if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
-      else rc = tc_mode<48, 48, 1, 256, 12>(P, grid, act, a.res, outw, acc_mode, s);
+      if (npb == 2 && a.ksize <= 3) rc = tc_mode<48, 48, 2, 256, 12, 3>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2 && a.ksize <= 7) rc = tc_mode<48, 48, 2, 256, 12, 7>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2) rc = tc_mode<48, 48, 2, 256, 12>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else rc = tc_mode<48, 48, 1, 256, 12>(P, diag, grid, act, a.res, outw, acc_mode, s);
     } else {
-      if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
-      else rc = tc_mode<24, 24, 1, 256, 6>(P, grid, act, a.res, outw, acc_mode, s);
+      if (npb == 2) rc = tc_mode<24, 24, 2, 256, 6>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else rc = tc_mode<24, 24, 1, 256, 6>(P, diag, grid, act, a.res, outw, acc_mode, s);
     }
   }
   if (rc) return rc;
@@ -747,11 +767,17 @@ extern "C" int alcm_opconv_dense(const alcm_opconv_args* args, alcm_stream_t str
                (hipStream_t)stream);
 }
 
-// diagnostics: the tconv phase trace (ALCM_XP3 = 1) summed since the last reset; reset zeroes it (stream-ordered on
-// the null stream)
+// diagnostics: the tconv phase trace (ALCM_TCONV_TRACE = 1) summed since the last reset; reset zeroes it.  The first
+// call allocates the trace buffer (zeroed, returns zeros; launches trace from then on).  Synchronizes the device.
 extern "C" int alcm_debug_tconv_trace(unsigned long long* out8, int reset) {
+  using namespace alcm;
+  if (!out8) return set_error(ALCM_E_INVALID, "debug_tconv_trace: null output");
   if (!alcm::g_tc_trace) {
     for (int i = 0; i < 8; ++i) out8[i] = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    ALCM_HIP(hipMalloc(&alcm::g_tc_trace, 512 * sizeof(unsigned long long)));
+    ALCM_HIP(hipMemset(alcm::g_tc_trace, 0, 512 * sizeof(unsigned long long)));
+    ALCM_HIP(hipDeviceSynchronize());
     return 0;
   }
   if (hipDeviceSynchronize() != hipSuccess) return -1;

@@ -281,9 +281,11 @@ int alcm_model_set_precision(alcm_model* m, int policy);
 int alcm_model_set_resblock_streams(alcm_model* m, int concurrent);
 /* re-read the ALCM_* diagnostic environment switches (they are read once at library load) */
 int alcm_reload_knobs(void);
-/* diagnostics: the BigVGAN tail-conv phase trace (ALCM_XP3=1): shader-clock cycles summed over waves and tiles for
- * [window + first slices, K loop, post-loop barrier, staging, residual + state, Activation1d, final barrier] and the
- * wave-tile count, since the last reset; reset != 0 zeroes it (synchronizes the device) */
+/* diagnostics: the BigVGAN tail-conv phase trace (ALCM_TCONV_TRACE=1, which selects the tail convs' diagnostics
+ * instantiations): shader-clock cycles summed over waves and tiles for [window + first slices, K loop, post-loop
+ * barrier, staging, residual + state, Activation1d, final barrier] and the wave-tile count, since the last reset;
+ * reset != 0 zeroes it.  The first call allocates the trace buffer and returns zeros (launches after it are traced).
+ * Synchronizes the device.  ALCM_E_INVALID for a null out8. */
 int alcm_debug_tconv_trace(unsigned long long* out8, int reset);
 
 /* DiT.  x (B,C_lat,T) NCT, t (B,) int64, ctx (B,154,1024), w_emb (B,256) -> eps (B,C_lat,T) NCT.

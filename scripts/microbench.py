@@ -329,12 +329,12 @@ def bench_tail1d(B=32):
 
 
 def bench_tphase(B=32):
-    """per-phase shader-clock breakdown of the tail convs as the model runs them (ALCM_XP3=1 trace): cycles per tile
+    """per-phase shader-clock breakdown of the tail convs as the model runs them (ALCM_TCONV_TRACE=1, the diagnostics instantiations): cycles per tile
     per wave of [window + first slices, K loop, post-loop barrier, stage v, residual + fp32 out, Activation1d, final
     barrier]; TCONFIGS = C:k:mode,... (mode conv1 / conv2)"""
     from audiolcm_amd.recipe import kaiser_sinc_filter1d
     f = kaiser_sinc_filter1d(0.25, 0.3, 12)
-    os.environ["ALCM_XP3"] = "1"
+    os.environ["ALCM_TCONV_TRACE"] = "1"
     _hip.reload_knobs()
     cfgs = os.environ.get("TCONFIGS", "96:3:conv2,96:11:conv2,96:11:conv1,48:3:conv2,48:11:conv2,24:3:conv2,24:11:conv2")
     for cfg in cfgs.split(","):
@@ -362,7 +362,7 @@ def bench_tphase(B=32):
             print(f"tphase C={C:3d} k={k:2d} {mode} xp={xv}: {ms:6.3f} ms  cycles/tile/wave [win kloop bar stage res act "
                   f"bar] {ph}  sum {sum(v[:7]) / tiles:7.0f}  wave-tiles {v[7]}", flush=True)
         os.environ.pop(os.environ.get("XP_NAME", "ALCM_XP0"))
-    os.environ.pop("ALCM_XP3")
+    os.environ.pop("ALCM_TCONV_TRACE")
     _hip.reload_knobs()
 
 
