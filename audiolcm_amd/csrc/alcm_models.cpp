@@ -1472,8 +1472,11 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     const bool dense = fuse && stage_tconv(S, pamp);
     const alcm_model::AuxSet* ax = S.rb.size() <= 3 ? voc_streams(m, s) : nullptr;
     const bool conc = ax != nullptr;
-    // the wide stages' conv1 -> Activation1d hand-off as an fp16 plane (ALCM_CONV1_H16=0: fp32, the A/B reference)
-    const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
+    // the wide stages' conv1 -> Activation1d hand-off as an fp16 plane (ALCM_CONV1_H16=0: fp32, the A/B reference).
+    // Only from B * To >= 1024 rows, where the fp32 route takes the same wide kernel (below it the fp32 output would
+    // go to opconv_kernel, whose K order differs): the A/B stays bit-exact at every size
+    const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp) &&
+                     (int64_t)B * To >= 1024;
     // the three chains' first Activation1d in one pass over u (their own planes, same taps)
     bool act3 = conc && fuse && S.rb.size() == 3 &&
                 !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);

@@ -292,7 +292,9 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
         const int64_t go = ((int64_t)b * P.orows + (int64_t)(r0 + m) * P.ostride + P.ooff) * P.N + col0 + n;
         float4 v = *reinterpret_cast<const float4*>(ot + m * OTS + n);
         v.x += bv[e].x; v.y += bv[e].y; v.z += bv[e].z; v.w += bv[e].w;
-        if (P.oplane) {  // plane output (no residual / accumulate / act): 4 rounded values, one 8-B store
+        if (P.oplane) {  // plane output (no residual / accumulate / act): 4 rounded values, one 8-B store; the
+          // residual-free + 0.f turns -0 into +0 exactly as the fp32 route's (v + 0) * 1 + 0 does
+          v.x += 0.f; v.y += 0.f; v.z += 0.f; v.w += 0.f;
           op_store2<PREC>(P.oplane + go, 0, f32x2{v.x, v.y});
           op_store2<PREC>(P.oplane + go + 2, 0, f32x2{v.z, v.w});
           continue;
