@@ -96,6 +96,7 @@ _SIGS = [
     ("alcm_model_set_resblock_streams", C.c_int, [vp, C.c_int]),
     ("alcm_reload_knobs", C.c_int, []),
     ("alcm_debug_tconv_trace", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
+    ("alcm_debug_tconv_wg_times", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     ("alcm_dit_workspace_bytes", C.c_size_t, [vp, C.c_int, C.c_int]),
     ("alcm_dit_embed_context", C.c_int, [vp, fp, C.c_int, fp, vp, C.c_size_t, vp]),
     ("alcm_dit_forward", C.c_int, [vp, fp, vp, fp, fp, fp, C.c_int, C.c_int, vp, C.c_size_t, vp]),
@@ -178,6 +179,16 @@ def debug_tconv_trace(reset: bool = True) -> list:
     out = (C.c_ulonglong * 8)()
     check(lib().alcm_debug_tconv_trace(out, 1 if reset else 0), "alcm_debug_tconv_trace")
     return list(out)
+
+
+def debug_tconv_wg_times(n_wg: int) -> list:
+    """Diagnostics: per-workgroup [entry, exit (s_memrealtime, 100 MHz), HW_ID, XCC_ID] of the last traced
+    resident-weight tail conv (alcm_debug_tconv_wg_times)."""
+    out = (C.c_ulonglong * (4 * n_wg))()
+    n = lib().alcm_debug_tconv_wg_times(out, n_wg)
+    if n < 0:
+        check(n, "alcm_debug_tconv_wg_times")
+    return [tuple(out[4 * i: 4 * i + 4]) for i in range(n)]
 
 
 PEAK_BF16_FLOPS = 2.5e15   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)

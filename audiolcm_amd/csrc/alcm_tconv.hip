@@ -90,6 +90,19 @@ struct TcTimer<false> {
   __device__ __forceinline__ void flush(unsigned long long*) {}
 };
 
+// diagnostics (DG, trace on): workgroup residency record — s_memrealtime at entry and exit, HW_ID and XCC_ID of its CU
+// (wave 0, lane 0; vector stores) at trace[512 + 4 * blockIdx.x ...] for blockIdx.x < TC_WG_REC
+constexpr int TC_WG_REC = 2048;
+__device__ __forceinline__ void tc_wg_record(unsigned long long* tr, int which) {
+  if (!tr || threadIdx.x != 0 || blockIdx.x >= TC_WG_REC) return;
+  unsigned long long* r = tr + 512 + 4 * blockIdx.x;
+  r[which] = __builtin_amdgcn_s_memrealtime();
+  if (which == 0) {
+    r[2] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+    r[3] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+  }
+}
+
 __device__ __forceinline__ void tc_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
 }
@@ -201,12 +214,14 @@ __device__ __forceinline__ void tc_window_tile(const TConvDev& P, int tile, int 
                    (uint32_t)((t0 - P.pad) * P.Cp * 2));
 }
 
-// weights bytes reserved for taps <= kmax: NSP rows x odd slots, rounded up to whole DMA instructions
+// weight rows held in LDS: the NS real rows, plus ONE zero row that every B-fragment lane of the padding columns
+// NS .. NSP-1 reads (a broadcast) when NS is not a multiple of 16
+static constexpr int tc_wrows(int NS) { return NS % 16 ? NS + 1 : NS; }
+// weights bytes reserved for taps <= kmax: tc_wrows rows x odd slots, rounded up to whole DMA instructions
 static constexpr int tc_wbytes(int C, int NS, int NPB, int kmax) {
-  const int nsp = (NS + 15) / 16 * 16;
   const int kd = (kmax * C + 31) / 32 * 32;
   const int slots = (kd / 8) % 2 ? kd / 8 : kd / 8 + 1;
-  return NPB * ((nsp * slots + 63) / 64) * 1024;
+  return NPB * ((tc_wrows(NS) * slots + 63) / 64) * 1024;
 }
 
 // C input channels, NS output channels per tile, NPB weight planes (1 = F16, 2 = F16W2), BM rows per tile,
@@ -217,9 +232,10 @@ static constexpr int tc_wbytes(int C, int NS, int NPB, int kmax) {
 // 25k-cycle tile); the loader's waits cover its own DMA only and the stores drain under the next tile's K loop.
 // Where the LDS holds the window apart from the staged tile (SEP: k <= 7 at C = 48), the loader DMAs the next tile's
 // window as soon as the K loop is done with the current one, under the epilogue.
+// OCC workgroups per CU (the launch bound on registers; the LDS must allow it too).
 // DG: the diagnostics instantiation (ablation bits, phase trace); false in production.
-template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC, bool DG>
-__global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P) {
+template <int C, int NS, int NPB, int BM, int R, int KMAX, int OCC, bool ACT, bool RES, bool OUTW, bool ACC, bool DG>
+__global__ __launch_bounds__(BM * 2 + 64, OCC == 1 ? 1 : (OCC * (BM / 32 + 1) + 3) / 4) void tconv_kernel(const TConvDev P) {
   constexpr int NW = BM / 32, NT = NW * 64;             // compute waves / threads
   constexpr int TM = 2, NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
   constexpr int RSS = (C / 8) % 2 ? C / 8 : C / 8 + 1;  // window row: odd number of 16-B slots
@@ -230,10 +246,10 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
   constexpr int STAGE = BM * OTS * 4;
   constexpr int WINB = WIN_INSTR * 1024;
   constexpr int WBYTES = tc_wbytes(C, NS, NPB, KMAX);
-  constexpr bool SEP = WBYTES + WINB + STAGE <= 163840;
+  constexpr bool SEP = WBYTES + WINB + STAGE <= 163840 / OCC;
   constexpr int REGION = SEP ? WINB + STAGE : (STAGE > WINB ? STAGE : WINB);
   constexpr int SMEM = WBYTES + REGION;
-  static_assert(SMEM <= 163840, "LDS");
+  static_assert(SMEM <= 163840 / OCC, "LDS: OCC workgroups per CU");
   static_assert(WIN_INSTR <= 60, "one wave's window DMA within the vmcnt range");
   static_assert((BM - 2 * ACT_EPI_HALO) % R == 0, "whole Activation1d runs (a partial run takes the clamped path)");
   static_assert(C % 8 == 0 && NS % 4 == 0, "geometry");
@@ -247,6 +263,7 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
   lds_char_t* const win3 = (lds_char_t*)win;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (DG) tc_wg_record(P.trace, 0);
   const int K = P.ksize, dil = P.dil;
   const int WS = P.wslots * 16;
   const int nslice = P.kd / 32;
@@ -255,8 +272,9 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
   const int E = BM - 2 * ACT_EPI_HALO;  // emitted rows per tile
 
   // ---- weights, once per workgroup (every wave): slot g of plane p -> row n = g / wslots, 16-B piece q = g % wslots
+  // (row NS, when present, is the zero row)
   {
-    const int total = NSP * P.wslots;
+    const int total = tc_wrows(NS) * P.wslots;
     const int instr = (total + 63) / 64;
     for (int p = 0; p < NPB; ++p) {
       for (int i = wave; i < instr; i += NW + 1) {
@@ -350,6 +368,9 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* arow = win + (wr0 + l16) * RS;
     const char* brow = wl + l16 * WS;
+    int bro[TN];  // B-fragment row offsets: row j * 16 + l16, or the zero row NS past the real columns
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bro[j] = (min(j * 16 + l16, NS) - l16) * WS;
     auto slice = [&](int s) {
       const int kk = s * 32 + q4 * 8;
       int tap = kk / C;
@@ -361,8 +382,8 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
         af[i] = *reinterpret_cast<const bf16x8*>(arow + (i * 16 + tap * dil) * RS + c * 2);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(brow + j * 16 * WS + kk * 2);
-        if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(brow + WBYTES / 2 + j * 16 * WS + kk * 2);
+        bh[j] = *reinterpret_cast<const bf16x8*>(brow + bro[j] + kk * 2);
+        if constexpr (NPB == 2) bl[j] = *reinterpret_cast<const bf16x8*>(brow + WBYTES / 2 + bro[j] + kk * 2);
       }
       if (DG && (P.ablate & 2)) {
 #pragma unroll
@@ -408,6 +429,7 @@ __global__ __launch_bounds__(BM * 2 + 64, 1) void tconv_kernel(const TConvDev P)
     tm.tile();
   }
   tm.flush(P.trace);
+  if constexpr (DG) tc_wg_record(P.trace, 1);
 }
 
 // Streamed-weight variant (ALCM_TCONV=2 / by shape): 4 waves of 64 rows x NS columns, the weights of each 32-deep K
@@ -593,7 +615,8 @@ __global__ __launch_bounds__(256, OCC) void tconv2_kernel(const TConvDev P) {
 }
 
 // -------------------------------------------------------------------------------------------------- host
-unsigned long long* g_tc_trace = nullptr;  // diagnostics trace buffer (64 x 8 sums), allocated by the first
+unsigned long long* g_tc_trace = nullptr;  // diagnostics trace buffer (64 x 8 sums + TC_WG_REC workgroup records),
+                                           // allocated by the first
                                            // alcm_debug_tconv_trace call (never inside a launch path)
 
 struct TConvCfg {
@@ -608,18 +631,18 @@ bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
   return C == 48 || C == 24;
 }
 
-template <int C, int NS, int NPB, int BM, int R, int KMAX, bool ACT, bool RES, bool OUTW, bool ACC>
+template <int C, int NS, int NPB, int BM, int R, int KMAX, int OCC, bool ACT, bool RES, bool OUTW, bool ACC>
 static void tc_launch(const TConvDev& P, bool diag, int grid, hipStream_t s) {
-  if (diag) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC, true>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
-  else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, ACT, RES, OUTW, ACC, false>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
+  if (diag) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, true>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
+  else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, false>), dim3(grid), dim3(BM * 2 + 64), 0, s, P);
 }
 
-template <int C, int NS, int NPB, int BM, int R, int KMAX = 11>
+template <int C, int NS, int NPB, int BM, int R, int KMAX = 11, int OCC = 1>
 static int tc_mode(const TConvDev& P, bool diag, int grid, bool act, bool res, bool outw, bool acc, hipStream_t s) {
   if (P.kd > (KMAX * C + 31) / 32 * 32) return set_error(ALCM_E_INVALID, "tconv: weights exceed the LDS reservation");
-  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, false, false, false>(P, diag, grid, s);
-  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, true, true, true, false>(P, diag, grid, s);
-  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, KMAX, false, true, false, true>(P, diag, grid, s);
+  if (act && !res && !outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, OCC, true, false, false, false>(P, diag, grid, s);
+  else if (act && res && outw && !acc) tc_launch<C, NS, NPB, BM, R, KMAX, OCC, true, true, true, false>(P, diag, grid, s);
+  else if (!act && res && acc) tc_launch<C, NS, NPB, BM, R, KMAX, OCC, false, true, false, true>(P, diag, grid, s);
   else return set_error(ALCM_E_INVALID, "tconv: unsupported epilogue combination");
   return 0;
 }
@@ -671,9 +694,13 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
   // streamed weights (two workgroups per CU) where the resident weights would take a CU's LDS: C >= 48
   const int tk = knobs().tconv;
   // measured per launch (scripts/microbench.py tconv): streamed wins at C = 96 and C = 24, resident at C = 48
-  const bool streamed = tk == 2 || (tk != 3 && C != 48);
-  const int BM = C == 96 ? 192 : 256;
-  const int NS = (!streamed && C == 96) ? 48 : C;
+  const bool streamed = tk == 2 || (tk != 3 && tk != 4 && C != 48);
+  // ALCM_TCONV=4 (C = 48): column halves (NS = 24, the B fragments of columns 24..31 read one zero row) on 128-row
+  // tiles, so the resident weights (k11: 54 KB) and the window leave room for two workgroups per CU
+  const bool half48 = !streamed && C == 48 && (tk == 4 || tk == 5);
+  const int occ48 = (tk == 5 && a.ksize <= 3) ? 3 : 2;  // ALCM_TCONV=5: k = 3 at three workgroups per CU
+  const int BM = C == 96 ? 192 : (half48 ? 128 : 256);
+  const int NS = (!streamed && C == 96) ? 48 : (half48 ? 24 : C);
   P.ncg = a.N / NS;
   P.tiles_per_batch = (a.T + (BM - 2 * ACT_EPI_HALO) - 1) / (BM - 2 * ACT_EPI_HALO);
   const int64_t nt = (int64_t)a.B * P.tiles_per_batch * P.ncg;
@@ -709,11 +736,18 @@ int tconv(const alcm_opconv_args& a, const u16* wd, int64_t wd_lo, int kd, const
     // tile it takes (tile % ncg == blockIdx % ncg); C = 24 fits two per CU
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int wgs = C == 24 ? 2 : 1;
+    const int wgs = half48 ? occ48 : (C == 24 ? 2 : 1);
     int grid = std::min<int64_t>(nt, (int64_t)ncu * wgs);
     grid = std::max(P.ncg, grid / P.ncg * P.ncg);
     if (C == 96) rc = tc_mode<96, 48, 1, 192, 11>(P, diag, grid, act, a.res, outw, acc_mode, s);
-    else if (C == 48) {
+    else if (half48) {
+      if (npb == 2 && a.ksize <= 3 && occ48 == 3)
+        rc = tc_mode<48, 24, 2, 128, 7, 3, 3>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2 && a.ksize <= 3) rc = tc_mode<48, 24, 2, 128, 7, 3, 2>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2 && a.ksize <= 7) rc = tc_mode<48, 24, 2, 128, 7, 7, 2>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else if (npb == 2) rc = tc_mode<48, 24, 2, 128, 7, 11, 2>(P, diag, grid, act, a.res, outw, acc_mode, s);
+      else rc = tc_mode<48, 24, 1, 128, 7, 11, 2>(P, diag, grid, act, a.res, outw, acc_mode, s);
+    } else if (C == 48) {
       // LDS weight region sized by the taps: k <= 7 leaves room for the window apart from the staged tile
       if (npb == 2 && a.ksize <= 3) rc = tc_mode<48, 48, 2, 256, 12, 3>(P, diag, grid, act, a.res, outw, acc_mode, s);
       else if (npb == 2 && a.ksize <= 7) rc = tc_mode<48, 48, 2, 256, 12, 7>(P, diag, grid, act, a.res, outw, acc_mode, s);
@@ -775,8 +809,9 @@ extern "C" int alcm_debug_tconv_trace(unsigned long long* out8, int reset) {
   if (!alcm::g_tc_trace) {
     for (int i = 0; i < 8; ++i) out8[i] = 0;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    ALCM_HIP(hipMalloc(&alcm::g_tc_trace, 512 * sizeof(unsigned long long)));
-    ALCM_HIP(hipMemset(alcm::g_tc_trace, 0, 512 * sizeof(unsigned long long)));
+    const size_t nb = (512 + 4 * TC_WG_REC) * sizeof(unsigned long long);
+    ALCM_HIP(hipMalloc(&alcm::g_tc_trace, nb));
+    ALCM_HIP(hipMemset(alcm::g_tc_trace, 0, nb));
     ALCM_HIP(hipDeviceSynchronize());
     return 0;
   }
@@ -789,4 +824,17 @@ extern "C" int alcm_debug_tconv_trace(unsigned long long* out8, int reset) {
   }
   if (reset && hipMemset(alcm::g_tc_trace, 0, sizeof(h)) != hipSuccess) return -1;
   return 0;
+}
+
+// diagnostics: the workgroup residency records of the last traced resident-weight tail conv (ALCM_TCONV_TRACE = 1):
+// per workgroup [entry s_memrealtime, exit s_memrealtime, HW_ID, XCC_ID] into out (4 x n_wg values); returns the
+// number of records copied (0 before the first alcm_debug_tconv_trace call).  Synchronizes the device.
+extern "C" int alcm_debug_tconv_wg_times(unsigned long long* out, int n_wg) {
+  using namespace alcm;
+  if (!out || n_wg < 0) return set_error(ALCM_E_INVALID, "debug_tconv_wg_times: bad arguments");
+  if (!alcm::g_tc_trace) return 0;
+  const int n = std::min(n_wg, TC_WG_REC);
+  ALCM_HIP(hipDeviceSynchronize());
+  ALCM_HIP(hipMemcpy(out, alcm::g_tc_trace + 512, (size_t)n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return n;
 }

@@ -287,6 +287,10 @@ int alcm_reload_knobs(void);
  * reset != 0 zeroes it.  The first call allocates the trace buffer and returns zeros (launches after it are traced).
  * Synchronizes the device.  ALCM_E_INVALID for a null out8. */
 int alcm_debug_tconv_trace(unsigned long long* out8, int reset);
+/* diagnostics: workgroup residency records of the last traced resident-weight tail conv (ALCM_TCONV_TRACE=1): per
+ * workgroup [entry s_memrealtime, exit s_memrealtime, HW_ID, XCC_ID] into out (4 x n_wg values, at most 2048
+ * workgroups); returns the count copied (0 before the first alcm_debug_tconv_trace call).  Synchronizes the device. */
+int alcm_debug_tconv_wg_times(unsigned long long* out, int n_wg);
 
 /* DiT.  x (B,C_lat,T) NCT, t (B,) int64, ctx (B,154,1024), w_emb (B,256) -> eps (B,C_lat,T) NCT.
  * cemb_cache: (B,154,hidden) device buffer filled by alcm_dit_embed_context (step-invariant, hoisted). */

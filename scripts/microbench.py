@@ -150,8 +150,12 @@ def bench_wone(B=32):
         o = torch.zeros((B, T, N), device="cuda") if acc else None
         pw = K.pack_conv_weight(w)
         pl = K.operand_planes(x, 2)
+        plane = os.environ.get("WONE_PLANE") == "1"  # the AMPBlock conv1 form: fp16 plane out, no residual
         for _ in range(5):
-            K.opconv(pl, Cin, w, None, d, 2, residual=r, packed=pw, accumulate_into=o)
+            if plane:
+                K.opconv(pl, Cin, w, None, d, 2, packed=pw, out_plane=True)
+            else:
+                K.opconv(pl, Cin, w, None, d, 2, residual=r, packed=pw, accumulate_into=o)
         torch.cuda.synchronize()
         print(f"{name}: done", flush=True)
 
@@ -366,6 +370,59 @@ def bench_tphase(B=32):
     _hip.reload_knobs()
 
 
+def bench_tres(B=32):
+    """workgroup residency of the resident-weight tail conv (ALCM_TCONV_TRACE=1 records): for TCONFIGS = C:k:mode and
+    each ALCM_TCONV in XP_VALS, how many workgroups were resident on one CU at once (max and mean over CUs), the
+    spread of entry times and the launch span"""
+    from audiolcm_amd.recipe import kaiser_sinc_filter1d
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12)
+    os.environ["ALCM_TCONV_TRACE"] = "1"
+    _hip.reload_knobs()
+    _hip.debug_tconv_trace()
+    for cfg in os.environ.get("TCONFIGS", "48:3:conv2,48:11:conv2").split(","):
+        C, k, mode = int(cfg.split(":")[0]), int(cfg.split(":")[1]), cfg.split(":")[2]
+        T = {96: 39936, 48: 79872, 24: 159744}[C]
+        d, p = (5 if k == 11 else 1), (2 if C == 96 else 3)
+        x = torch.randn((B, T, C), device="cuda")
+        r = torch.randn((B, T, C), device="cuda")
+        a, bt = torch.randn(C, device="cuda") * 0.3, torch.randn(C, device="cuda") * 0.3
+        pl = K.operand_planes(x, p)
+        w = torch.randn((C, C, k), device="cuda") * (0.5 / (C * k) ** 0.5)
+        pd = K.pack_conv_weight(w)
+        conv2 = mode == "conv2"
+        for xv in os.environ.get("XP_VALS", "1").split(","):
+            os.environ["ALCM_TCONV"] = xv
+            _hip.reload_knobs()
+            run = lambda: K.opconv(pl, C, w, None, d, p, residual=r if conv2 else None, packed=pd, act=(a, bt, f, f),
+                                   fp32_out=conv2, dense=True)
+            run()
+            torch.cuda.synchronize()
+            recs = [x for x in _hip.debug_tconv_wg_times(2048) if x[1] > x[0] > 0]
+            if not recs:
+                print(f"tres C={C} k={k} {mode} tconv={xv}: no records (streamed kernel?)", flush=True)
+                continue
+            t0 = min(x[0] for x in recs)
+            per = {}
+            for s_, e_, hw, xcc in recs:
+                per.setdefault((xcc, (hw >> 8) & 0xFF), []).append((s_ - t0, e_ - t0))
+            conc = []
+            for iv in per.values():
+                ev = sorted([(s_, 1) for s_, _ in iv] + [(e_, -1) for _, e_ in iv], key=lambda z: (z[0], z[1]))
+                cur = best = 0
+                for _, dlt in ev:
+                    cur += dlt
+                    best = max(best, cur)
+                conc.append(best)
+            span = max(x[1] for x in recs) - t0
+            starts = sorted(x[0] - t0 for x in recs)
+            print(f"tres C={C} k={k} {mode} tconv={xv}: {len(recs)} WGs on {len(per)} CUs, resident per CU max "
+                  f"{max(conc)} mean {sum(conc) / len(conc):.2f}; entry spread {starts[-1] / 100:.1f} us (median "
+                  f"{starts[len(starts) // 2] / 100:.1f}), launch span {span / 100:.1f} us", flush=True)
+        os.environ.pop("ALCM_TCONV")
+    os.environ.pop("ALCM_TCONV_TRACE")
+    _hip.reload_knobs()
+
+
 def bench_tail1(B=32):
     """3 launches of the stage-4 (C = 48, k = 11, d = 5, F16W2) conv2 + residual + fused Activation1d as the model
     runs it, with the current ALCM_* settings (target of rocprofv3 --pmc passes)"""
@@ -452,4 +509,4 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["op", "conv", "act"]
     spin(float(os.environ.get("SPIN", "3")))
     for w in which:
-        {"tphase": bench_tphase, "xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()
+        {"tres": bench_tres, "tphase": bench_tphase, "xp": bench_xp, "h16": bench_h16, "text": bench_text, "tail1d": bench_tail1d, "tconv": bench_tconv, "tail1": bench_tail1, "attn": bench_attn, "act1": bench_act1, "wone": bench_wone, "op": bench_op, "op1": bench_op1, "conv": bench_conv, "wconv": bench_wconv, "tail": bench_tail, "ffn": bench_ffn, "act": bench_act, "conv1": bench_conv_one}[w]()

@@ -7,7 +7,7 @@ import sys
 
 d, pat = sys.argv[1], sys.argv[2]
 agg, n = collections.defaultdict(float), collections.Counter()
-for f in sorted(glob.glob(f"{d}/*/run_counter_collection.csv") + glob.glob(f"{d}/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{d}/*/run_counter_collection.csv") + glob.glob(f"{d}/run_counter_collection.csv") + glob.glob(f"{d}/compact.csv")):
     for r in csv.DictReader(open(f)):
         if pat in r.get("Kernel_Name", ""):
             agg[r["Counter_Name"]] += float(r["Counter_Value"])

@@ -722,10 +722,14 @@ def test_opconv_dense_resident_weights(K, C, T, k, dil, prec, mode):
         assert rel_l2(o_d.cpu().numpy(), o_ref.cpu().numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("C,k,dil,mode", [(48, 11, 5, "conv2"), (48, 7, 3, "conv2"), (48, 3, 1, "conv1"),
-                                          (24, 3, 1, "conv2"), (24, 11, 5, "conv1"), (96, 11, 5, "conv2"),
-                                          (48, 11, 5, "last")])
-def test_tail_conv_multitile_vs_oracle(K, C, k, dil, mode):
+@pytest.mark.parametrize("C,k,dil,mode,tk", [(48, 11, 5, "conv2", "1"), (48, 7, 3, "conv2", "1"), (48, 3, 1, "conv1", "1"),
+                                             (24, 3, 1, "conv2", "1"), (24, 11, 5, "conv1", "1"), (96, 11, 5, "conv2", "1"),
+                                             (48, 11, 5, "last", "1"),
+                                             # C = 48 column halves on 128-row tiles, two / three workgroups per CU
+                                             (48, 11, 5, "conv2", "4"), (48, 7, 3, "conv1", "4"), (48, 3, 1, "conv2", "4"),
+                                             (48, 3, 1, "conv2", "5"), (48, 3, 1, "conv1", "5"), (48, 11, 5, "last", "4"),
+                                             (48, 3, 1, "last", "5")])
+def test_tail_conv_multitile_vs_oracle(K, C, k, dil, mode, tk, monkeypatch):
     """The narrow AMPBlock convs (vocoder/bigvgan/models.py:72-81, stages 3-5) on > 256 tiles — persistent resident
     workgroups walking several tiles with the loader wave's next-window prefetch (C = 48), four streamed workgroups
     per CU (C = 24), the C = 96 persistent streamed grid — against the fp32 ORACLE, not another HIP kernel:
@@ -747,6 +751,18 @@ def test_tail_conv_multitile_vs_oracle(K, C, k, dil, mode):
     if mode != "conv1":
         ref = ref + r.permute(0, 2, 1)
     act = (dev(a), dev(bt), f, f)
+    from audiolcm_amd import _hip
+    monkeypatch.setenv("ALCM_TCONV", tk)
+    _hip.reload_knobs()
+    try:
+        _tail_run_and_check(K, C, k, dil, mode, prec, pl, w, bias, r, a, bt, f, act, ref, B, T)
+    finally:
+        monkeypatch.delenv("ALCM_TCONV")
+        _hip.reload_knobs()
+
+
+def _tail_run_and_check(K, C, k, dil, mode, prec, pl, w, bias, r, a, bt, f, act, ref, B, T):
+    from oracle import alcm_oracle as O
     if mode == "conv1":
         _, pl_d = K.opconv(pl, C, dev(w), dev(bias), dil, prec, act=act, fp32_out=False, dense=True)
     elif mode == "conv2":
