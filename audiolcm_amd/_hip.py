@@ -51,7 +51,8 @@ class OpConvArgs(C.Structure):
                 ("accumulate", C.c_int), ("out_scale", C.c_float), ("prec", C.c_int),
                 ("act_plane", vp), ("act_plane_lo_off", i64), ("act_alpha_exp", fp), ("act_inv_beta", fp),
                 ("act_up_filter", fp), ("act_down_filter", fp), ("geglu_plane", vp),
-                ("out_stride", C.c_int), ("out_offset", C.c_int), ("out_rows", C.c_int), ("out_plane", vp)]
+                ("out_stride", C.c_int), ("out_offset", C.c_int), ("out_rows", C.c_int), ("out_plane", vp),
+                ("ksplit_ws", fp), ("ksplit_ws_floats", i64)]
 
 
 class NamedTensor(C.Structure):

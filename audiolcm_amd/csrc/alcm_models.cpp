@@ -700,6 +700,8 @@ struct Bump {
 // ------------------------------------------------------------------ DiT
 struct DitWs {
   float *h, *u, *o, *qkv, *S, *g, *mean, *rstd, *gsc, *gsh, *tv, *tf, *t1;
+  float* kp;  // K-split partial sums of the FFN down-projection (4 parts)
+  int64_t kp_floats;
 };
 static DitWs plan_dit(const DitW& D, Bump& bp, int B, int T) {
   const int H = D.hidden, L = 1 + D.ctx_tokens + T, Lp = round_up(L, 8);
@@ -717,6 +719,8 @@ static DitWs plan_dit(const DitW& D, Bump& bp, int B, int T) {
   w.tv = bp.take<float>((size_t)B);
   w.tf = bp.take<float>((size_t)B * 256);
   w.t1 = bp.take<float>((size_t)B * H);
+  w.kp_floats = (int64_t)4 * B * L * H;
+  w.kp = bp.take<float>((size_t)w.kp_floats);
   return w;
 }
 
@@ -907,6 +911,8 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
       g.ksize = D.ff_k; g.dil = 1; g.pad = D.ff_k / 2;
       g.w = blk.ff2.w.p; g.w_lo_off = blk.ff2.w.lo; g.kpad = blk.ff2.w.kpad; g.N = blk.ff2.w.rows;
       g.bias = blk.ff2.b; g.res = w.u; g.out = w.u; g.out_scale = 1.f; g.prec = pff;
+      // 192 tiles of 256 x 192 at B = 32: K parts fill the chip (alcm_wconv.hip wconv3_parts)
+      g.ksplit_ws = w.kp; g.ksplit_ws_floats = w.kp_floats;
       ALCM_TRY(opconv(g, s));
     } else {
       ALCM_TRY(row_stats(w.u, B * L, H, H, 1e-5f, w.mean, w.rstd, s));

@@ -39,6 +39,9 @@ struct WConvDev {
   u16* gplane;          // GEGLU epilogue: operand plane [B][T][N/2] instead of the fp32 output
   int out_act;          // wconv2: activation of acc + bias (ALCM_ACT_*, 0 = none)
   u16* oplane;          // wconv2: conv + bias as an operand plane [B][T][N] (PREC) instead of the fp32 output
+  int ksplit;           // wconv3: > 1 = the 64-channel chunks split into ksplit contiguous parts, one work item per
+                        // (tile, part); each item writes its fp32 partial sums to part + kpart * B T N (no epilogue)
+  float* part;
 };
 
 
@@ -358,19 +361,25 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   const int wm = wave >> 1, wn = wave & 1;
 
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  // work items: tiles, or (K split) (part, tile) pairs part-major, so an XCD's contiguous item range walks the
+  // tiles of one part as the unsplit kernel walks its tiles
+  const int KS = P.ksplit > 1 ? P.ksplit : 1;
   const int ntiles = P.nwg;
-  const int R = (ntiles + 7) >> 3;
-  const int tbeg = xcd * R, tend = min(tbeg + R, ntiles);
+  const int nitems = ntiles * KS;
+  const int R = (nitems + 7) >> 3;
+  const int tbeg = xcd * R, tend = min(tbeg + R, nitems);
   const int first = tbeg + slot;
   const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
   if (my_n == 0) return;
-  const int K = P.ksize, Cp = P.Cp, nC = Cp / 64;
+  const int K = P.ksize, Cp = P.Cp, nC = Cp / 64 / KS;  // 64-channel chunks per item
   const int WR = W3_BM + (K - 1) * P.dil;
   const int total = my_n * nC * K;   // steps
   const int nchunks = my_n * nC;     // windows
   const int tiles_m = ntiles / P.tiles_n;
-  auto tile_of = [&](int ti, int& b, int& t0, int& col0) {
-    const int tile = first + ti * nslot;
+  auto tile_of = [&](int ti, int& b, int& t0, int& col0, int& kp) {
+    int tile = first + ti * nslot;
+    kp = tile / ntiles;  // K part (0 unless split)
+    tile -= kp * ntiles;
     int mt, nt;
     if (P.n_major) {
       nt = tile / tiles_m;
@@ -390,9 +399,9 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   int wbuf = 0;
   auto win_setup = [&](int q) {
     const int ti = q / nC, c = q - ti * nC;
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
-    wsrc_base = P.a + (int64_t)b * P.T * Cp + c * 64;
+    int b, t0, col0, kp;
+    tile_of(ti, b, t0, col0, kp);
+    wsrc_base = P.a + (int64_t)b * P.T * Cp + (kp * nC + c) * 64;
     wrow0 = t0 - P.pad;
     wbuf = q & 1;
   };
@@ -430,9 +439,9 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   int ig = 0, ic = 0, itap = 0, iti = 0;
   int64_t iwoff;
   {
-    int b_, t0_, col0_;
-    tile_of(0, b_, t0_, col0_);
-    iwoff = (int64_t)col0_ * P.kpad;
+    int b_, t0_, col0_, kp_;
+    tile_of(0, b_, t0_, col0_, kp_);
+    iwoff = (int64_t)col0_ * P.kpad + kp_ * nC * 64;
   }
   auto issue_wt = [&](int sl) {
     const char* base = reinterpret_cast<const char*>(P.w + iwoff);
@@ -447,9 +456,9 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
       iwoff += 64 - (int64_t)K * Cp;
       if (++ic == nC) {
         ic = 0;
-        int b_, t0_, col0_;
-        tile_of(++iti, b_, t0_, col0_);
-        iwoff = (int64_t)col0_ * P.kpad;
+        int b_, t0_, col0_, kp_;
+        tile_of(++iti, b_, t0_, col0_, kp_);
+        iwoff = (int64_t)col0_ * P.kpad + kp_ * nC * 64;
       }
     }
   };
@@ -477,11 +486,18 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   // operand plane of acc + bias in the format of PREC (the AMPBlock conv1 whose only consumer, the next Activation1d,
   // rounds its input to that format: the same rounding of the same fp32 value, half the bytes on both sides)
   auto epilogue = [&](int ti) {
-    int b, t0, col0;
-    tile_of(ti, b, t0, col0);
+    int b, t0, col0, kp;
+    tile_of(ti, b, t0, col0, kp);
+    // K split: this part's raw sums into its partial slice (bias / residual / scale / accumulate in the reduction)
+    const bool split = KS > 1;
+    float* const outp = split ? P.part + (int64_t)kp * ((int64_t)(P.nwg / P.tiles_n / P.tiles_per_batch) * P.T * P.N)
+                              : P.out;
+    const float* const resp = split ? nullptr : P.res;
+    const bool accum = !split && P.accumulate;
+    const float oscale = split ? 1.f : P.out_scale;
     float bv[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bv[j] = P.bias ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
+    for (int j = 0; j < TN; ++j) bv[j] = (P.bias && !split) ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
     if (P.oplane) {
       // column pairs through a lane-pair exchange (DPP quad_perm [1, 0, 3, 2]): per accumulator row pair (r0, r1) the
       // even lane of a pair stores row r0, columns (c, c + 1), the odd lane row r1, columns (c - 1, c): 4-B stores
@@ -517,8 +533,8 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          rv[r][j] = P.res ? P.res[ro + j * 16] : 0.f;
-          pv[r][j] = P.accumulate ? P.out[ro + j * 16] : 0.f;
+          rv[r][j] = resp ? resp[ro + j * 16] : 0.f;
+          pv[r][j] = accum ? outp[ro + j * 16] : 0.f;
         }
       }
 #pragma unroll
@@ -527,7 +543,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          P.out[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * P.out_scale + pv[r][j];
+          outp[ro + j * 16] = (acc[i][j][r] + bv[j] + rv[r][j]) * oscale + pv[r][j];
       }
     }
   };
@@ -640,9 +656,54 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
 
 static int g_ncu = 0;
 
+// K-split reduction of wconv3's partial slices: out = (sum over parts, in part order, + bias + res) * scale (+ out) —
+// the unsplit epilogue's expression with its accumulator replaced by the ordered part sum, so a launch is
+// deterministic (bit-stable run to run); float4 per lane over the B T N / 4 outputs (N % 4 == 0)
+__global__ __launch_bounds__(256) void ksplit_reduce_kernel(const float4* __restrict__ part, int ks, int64_t n4, int N4,
+                                                            const float4* __restrict__ bias, const float4* res,
+                                                            float4* out, float scale, int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 a = part[i];
+    for (int p = 1; p < ks; ++p) {
+      const float4 v = part[(int64_t)p * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const float4 bv = bias ? bias[i % N4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 rv = res ? res[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 pv = accumulate ? out[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 o;
+    o.x = (a.x + bv.x + rv.x) * scale + pv.x;
+    o.y = (a.y + bv.y + rv.y) * scale + pv.y;
+    o.z = (a.z + bv.z + rv.z) * scale + pv.z;
+    o.w = (a.w + bv.w + rv.w) * scale + pv.w;
+    out[i] = o;
+  }
+}
+
+// K parts for wconv3 on a grid that does not fill the chip (items = tiles x parts): the smallest part count that
+// minimises rounds-of-items per part (e.g. the DiT FFN down-projection: 192 tiles of 256 x 192 on 256 CUs, 0.75 busy;
+// 4 parts = 768 items = 3 per CU, 0.75 of the time plus the reduction), within the caller's partial workspace; 1 =
+// no split
+static int wconv3_parts(const alcm_opconv_args& a, int64_t tiles, int ncu) {
+  if (!a.ksplit_ws || knobs().ksplit == 0 || a.out_plane || a.Cp % 64) return 1;
+  const int nc = a.Cp / 64;
+  int ks = 1;
+  double best = (double)((tiles + ncu - 1) / ncu);
+  for (int k = 2; k <= 8; ++k) {
+    if (nc % k || (double)k * a.B * a.T * a.N > (double)a.ksplit_ws_floats) continue;
+    const double t = (double)((tiles * k + ncu - 1) / ncu) / k;
+    if (t < best * 0.95) {
+      best = t;
+      ks = k;
+    }
+  }
+  return ks;
+}
+
 // Eligible: fp16 / bf16 operands, Cp % 64 == 0, 3 <= k, (k-1) d <= 64, N % 192 == 0, plain fp32 epilogue (bias,
 // residual, scale, accumulate; no GEGLU / strided output).  Returns 1 when it launched.
-static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s) {
+static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops, double bytes, hipStream_t s,
+                      int ks = 1) {
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;
   if (a.out_act || a.out_stride > 0 || a.geglu_plane || a.Cp % 64 || a.ksize < 3 || (a.ksize - 1) * a.dil > 64 ||
       a.N % W3_BN)
@@ -669,15 +730,30 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if ((int64_t)W3_BN * a.kpad * 2 >= (1ll << 31)) return 0;  // per-lane 32-bit weight-row byte offsets
   P.nwg = (int)nt;
   P.n_major = 1;
-  const int R = (P.nwg + 7) / 8;
+  if (ks > 1) {
+    if (a.out_plane || (a.Cp / 64) % ks || (int64_t)a.N % 4 || (((uintptr_t)a.ksplit_ws) & 15) ||
+        (a.bias && (((uintptr_t)a.bias) & 15)) || (a.res && (((uintptr_t)a.res) & 15)) || (((uintptr_t)a.out) & 15))
+      return 0;
+    P.ksplit = ks;
+    P.part = a.ksplit_ws;
+  }
+  const int R = (int)((nt * ks + 7) / 8);
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
   if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
   else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
+  if (ks > 1) {
+    const int64_t n4 = (int64_t)a.B * a.T * a.N / 4;
+    const unsigned rg = (unsigned)std::min<int64_t>((n4 + 255) / 256, (int64_t)g_ncu * 8);
+    hipLaunchKernelGGL(ksplit_reduce_kernel, dim3(rg), dim3(256), 0, s, reinterpret_cast<const float4*>(a.ksplit_ws),
+                       ks, n4, a.N / 4, reinterpret_cast<const float4*>(a.bias), reinterpret_cast<const float4*>(a.res),
+                       reinterpret_cast<float4*>(a.out), a.out_scale, a.accumulate);
+  }
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d>", a.prec);
+    std::snprintf(name, sizeof(name), ks > 1 ? "alcm::wconv3_kernel<%d> + ksplit_reduce" : "alcm::wconv3_kernel<%d>",
+                  a.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -717,10 +793,14 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
                 ? n
                 : 256;
   }
-  const bool fills = (int64_t)a.B * mt256 * (a.N / W3_BN) >= g_ncu;
+  const int64_t tiles3 = (int64_t)a.B * mt256 * (a.N / W3_BN);
+  const bool fills = tiles3 >= g_ncu;
+  // a grid that does not fill the chip: K parts where the caller gave a partial workspace (ALCM_KSPLIT=0: never)
+  const int ks = (!off && w3 != 0 && full && !fills && !strided && !a.geglu_plane && a.N % W3_BN == 0)
+                     ? wconv3_parts(a, tiles3, g_ncu) : 1;
   if (!off && (a.out_plane || (int64_t)a.B * a.T >= 1024) && lin_plane_try(a, wplane, flops, bytes, s)) return 1;
-  if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || (full && fills)) &&
-      wconv3_try(a, wplane, flops, bytes, s))
+  if (!off && w3 != 0 && !strided && !a.geglu_plane && (w3 > 0 || (full && (fills || ks > 1))) &&
+      wconv3_try(a, wplane, flops, bytes, s, ks))
     return 1;
   if (off && !a.geglu_plane && !strided && !a.out_plane) return 0;
   if (a.prec != PREC_F16 && a.prec != PREC_BF16) return 0;

@@ -362,7 +362,8 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,
            act: Optional[tuple] = None, fp32_out: bool = True, geglu: bool = False,
-           strided: Optional[tuple] = None, dense: bool = False, out_plane: bool = False):
+           strided: Optional[tuple] = None, dense: bool = False, out_plane: bool = False,
+           ksplit_ws: Optional[torch.Tensor] = None):
     """Same-length conv1d (B, T, N) = conv_{k,dilation}(operand planes (NP, B, T, Cp)) + bias (+res ...).
 
     act = (alpha, beta, up_filter, down_filter): also return Activation1d(conv + bias (+res)) as operand
@@ -372,7 +373,8 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     dense = True: the narrow-stage resident-weight kernel (alcm_opconv_dense): weights packed with cpad = C_real
     (pack_conv_weight(w)), planes channels >= C_real ignored, the fused Activation1d writes channels < N only.
     out_plane = True: conv + bias as one PREC operand plane (1, B, T, N) instead of the fp32 output (no residual /
-    activation / accumulate; the DiT q,k,v projection)."""
+    activation / accumulate; the DiT q,k,v projection).
+    ksplit_ws: fp32 device workspace the library may use for K-split partial sums (alcm_opconv_args.ksplit_ws)."""
     npl, B, T, Cp = planes.shape
     assert planes.dtype == torch.int16 and planes.is_contiguous()
     N, cin, k = w.shape
@@ -387,6 +389,9 @@ def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[to
     a.ksize, a.dil, a.pad = k, dilation, (k - 1) * dilation // 2
     a.w, a.w_lo_off, a.kpad, a.N = ptr(packed.data), packed.lo_off, packed.kpad, N
     a.bias = ptr(bias)
+    if ksplit_ws is not None:
+        assert ksplit_ws.dtype == torch.float32 and ksplit_ws.is_contiguous()
+        a.ksplit_ws, a.ksplit_ws_floats = ptr(ksplit_ws), ksplit_ws.numel()
     if strided is not None:
         out, a.out_stride, a.out_offset, a.pad = strided
         assert out.is_contiguous() and out.shape[0] == B and out.shape[2] == N

@@ -215,6 +215,13 @@ typedef struct alcm_opconv_args {
    * that format anyway (the DiT q/k/v projection feeding the fused attention).  Needs the wide-layer kernel
    * (F16 / BF16, N % 4 == 0, Cp % 64 == 0) and no res / accumulate / out_act / act / GEGLU / strided output. */
   void* out_plane;
+  /* optional K-split workspace (fp32, 16-byte aligned, ksplit_ws_floats floats): where the persistent wide-layer
+   * kernel's grid would not fill the chip (the DiT FFN down-projection: 192 tiles of 256 x 192 on 256 CUs), the
+   * library may split the 64-channel K chunks into P parts (P * B * T * N <= ksplit_ws_floats), write P fp32
+   * partial slices here and reduce them in part order with the bias / residual / scale / accumulate epilogue (a
+   * second launch on the same stream): deterministic, not bit-identical to the unsplit sum.  NULL: never split. */
+  float* ksplit_ws;
+  int64_t ksplit_ws_floats;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
 /* alcm_opconv_dense: the narrow AMPBlock conv of BigVGAN stages 3-5 (vocoder/bigvgan/models.py:72-81, C = N in

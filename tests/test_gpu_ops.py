@@ -856,3 +856,43 @@ def test_conv1_fp16_handoff(K, C, T, k, dil, grid, monkeypatch):
         else:
             assert rel_l2(y16.cpu()[0].view(torch.float16).float().numpy(), y32.cpu().numpy()) < 1e-3
         assert torch.equal(act16, act32), f"activation on the fp16 plane differs, wconv3={w3}"
+
+
+@pytest.mark.parametrize("B,acc", [(4, False), (8, True)])
+def test_wconv3_ksplit_underfilled(K, B, acc, monkeypatch):
+    """K-split persistent wide conv on a grid that does not fill the chip (the DiT FFN down-projection shape, k9
+    2304 -> 576 at L = 467: 6 B tiles of 256 x 192; new_attention.py:48-55 / concatDiT.py FeedForward): partial sums
+    per K part + the ordered reduction with bias / residual / scale (/ accumulate).  vs the unsplit launch (fp32
+    summation order only: rel-L2 1e-6), vs F.conv1d on the fp16 operands, and bit-stable across runs."""
+    from audiolcm_amd import _hip
+    T, C, N, k = 467, 2304, 576, 9
+    x = _r((B, T, C), 170, 0.5)
+    w, bias = _r((N, C, k), 171, 1.0 / np.sqrt(C * k)), _r((N,), 172, 0.05)
+    r = _r((B, T, N), 173)
+    o0 = _r((B, T, N), 174)
+    pl = K.operand_planes(dev(x), 2)
+    pw = K.pack_conv_weight(dev(w))
+    ws = torch.empty(8 * B * T * N, device="cuda")
+
+    def run(split):
+        o = dev(o0.clone()) if acc else None
+        y = K.opconv(pl, C, dev(w), dev(bias), 1, 2, residual=dev(r), packed=pw, out_scale=0.5,
+                     accumulate_into=o, ksplit_ws=ws if split else None)
+        return y.cpu()
+    monkeypatch.setenv("ALCM_PROF_SHAPES", "1")
+    _hip.reload_knobs()
+    _hip.profile_begin()
+    ys = run(True)
+    torch.cuda.synchronize()
+    prof = _hip.profile_end()
+    monkeypatch.delenv("ALCM_PROF_SHAPES")
+    _hip.reload_knobs()
+    assert any("ksplit_reduce" in p["name"] for p in prof), [p["name"] for p in prof]
+    y1 = run(False)
+    assert torch.equal(ys, run(True)), "K-split result not bit-stable"
+    ref = (F.conv1d(x.half().float().permute(0, 2, 1), w.half().float(), bias, padding=k // 2).permute(0, 2, 1) + r) * 0.5
+    if acc:
+        ref = ref + o0
+    e_s, e_1 = rel_l2(ys.numpy(), y1.numpy()), rel_l2(ys.numpy(), ref.numpy())
+    print(f"ksplit B{B}: split vs unsplit {e_s:.2e}, vs F.conv1d {e_1:.2e}")
+    assert e_s < 1e-6 and e_1 < 1e-5
