@@ -129,6 +129,8 @@ def lib() -> C.CDLL:
                               "(make -C audiolcm_amd/csrc). The MI355X path has no CPU fallback.")
         L = C.CDLL(LIB_PATH)
         for name, res, args in _SIGS:
+            if name.startswith("alcm_debug_") and "ALCM_LIB" in os.environ and not hasattr(L, name):
+                continue  # an older library loaded for an A/B (ALCM_LIB) may predate a diagnostics entry
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

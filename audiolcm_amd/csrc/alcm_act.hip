@@ -80,33 +80,26 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   const int j0 = t0 + run * 8;
   const int jn = min(8, T - j0);
 
-  // ---- phase 1a: the upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
-  //      x-window offsets are compile-time), once for all NSET parameter sets: UpSample1d does not depend on the
-  //      SnakeBeta parameters (the three resblocks' first Activation1d differ only there), so the up FIR runs once,
-  //      not NSET times (act_coop_kernel<.., 3> issued 3x the up-FIR packed FMAs: 687 vs 229 per thread)
-  // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer order compiles
-  // to 6-deep dependent chains with a wait state between links)
-  f32x2 u[AC_SEG];
-  if (live && interior) {
-#pragma unroll
-    for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk)
-#pragma unroll
-      for (int q = 0; q < AC_SEG; ++q) {
-        const int ku = 2 * kk + ((q & 1) ? 0 : 1);
-        u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
-      }
-  }
-
 #pragma unroll
   for (int st = 0; st < NSET; ++st) {
     const f32x2 ear = live ? f32x2{S.aexp[st][c], S.aexp[st][c + 1]} * INV_PI : f32x2{0.f, 0.f};
     const f32x2 h = live ? f32x2{S.ibeta[st][c], S.ibeta[st][c + 1]} * 0.5f : f32x2{0.f, 0.f};
-    // ---- phase 1b: SnakeBeta of this set on the upsampled samples; replicate padding = the sample at the clamped
-    //      index (edge segments recompute their samples per set)
+    // ---- phase 1: upsampled samples mb .. mb + 17 of segment seg (mb even, so the polyphase tap parity and the
+    //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
     if (live) {
       if (interior) {
+        // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
+        // order compiles to 6-deep dependent chains with a wait state between links)
+        f32x2 u[AC_SEG];
+#pragma unroll
+        for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+          for (int q = 0; q < AC_SEG; ++q) {
+            const int ku = 2 * kk + ((q & 1) ? 0 : 1);
+            u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
+          }
 #pragma unroll
         for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
       } else {

@@ -395,6 +395,7 @@ def bench_tres(B=32):
             _hip.reload_knobs()
             run = lambda: K.opconv(pl, C, w, None, d, p, residual=r if conv2 else None, packed=pd, act=(a, bt, f, f),
                                    fp32_out=conv2, dense=True)
+            _hip.debug_tconv_trace()  # reset: records of earlier (larger) grids cleared
             run()
             torch.cuda.synchronize()
             recs = [x for x in _hip.debug_tconv_wg_times(2048) if x[1] > x[0] > 0]
