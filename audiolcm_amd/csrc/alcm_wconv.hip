@@ -68,10 +68,7 @@ constexpr int W2_HALO = 64;  // max (k - 1) * dil
 
 // BM = 160 (waves 2 x 2 of 80 x 96, TM = 5): sequences of T = 312 rows as two tiles (320 rows) instead of three of 128
 // (384 rows, 768 tiles on the 512 workgroup slots of the chip: the VAE's k3 convs)
-// NB weight buffers: 2 (step s + 1 staged while step s computes, vmcnt(0) at every step end) or 3 (256 x 96 tiles,
-// whose 12 KB weight images leave room for a third within the two-workgroup LDS budget: step s + 2 is staged while step
-// s computes and each step end waits only for step s + 1, vmcnt(BPW), so a weight tile has two steps to land)
-template <int PREC, bool GEGLU, int BM = 128, int BN = 192, int NB = 2>
+template <int PREC, bool GEGLU, int BM = 128, int BN = 192>
 __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int WGM = BM == 256 ? 4 : 2, WGN = 4 / WGM;  // wave grid
   constexpr int TM = BM / WGM / 16, TN = 6;
@@ -80,8 +77,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
   constexpr int WROWS = BM + W2_HALO;
   constexpr int WBUF = WROWS * 128;      // window image
   constexpr int BBUF = BN * 128;         // weight image
-  constexpr int SMEM = WBUF + NB * BBUF;  // 72 KB (128 x 192) / 64 (256 x 96; 76 with NB = 3) / 76 KB (160 x 192)
-  static_assert(SMEM <= 81920, "two workgroups per CU");
+  constexpr int SMEM = WBUF + 2 * BBUF;  // 72 KB (128 x 192) / 64 KB (256 x 96) / 76 KB (160 x 192)
   constexpr int WPW = WROWS / 8 / 4;     // window DMA instructions per wave (6 / 10 / 7)
   static_assert(WROWS % 32 == 0, "whole window DMA instructions per wave");
   constexpr int BPW = BN / 8 / 4;        // weight DMA instructions per wave per step (6 / 3)
@@ -151,14 +147,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
 
     stage_w(0);
     stage_b(0, 0);
-    if constexpr (NB == 3) {
-      if (steps > 1) stage_b(1, 1);
-      static_assert(BPW == 3, "vmcnt immediate below");
-      if (steps > 1) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");  // window + step 0 landed
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     {
       // fragment-pipelined K loop: the second 32-deep slice's fragments are read
       // while the first slice's MFMAs run (B fragments as their last use retires, A fragments after each row),
@@ -179,12 +168,8 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
       int st = 0;
       for (int c = 0; c < nC; ++c) {
         for (int tap = 0; tap < K; ++tap, ++st) {
-          if constexpr (NB == 3) {
-            if (st + 2 < steps) stage_b(st + 2, (st + 2) % 3);
-          } else {
-            if (st + 1 < steps) stage_b(st + 1, (st + 1) & 1);
-          }
-          const char* Bl = smem + WBUF + (NB == 3 ? st % 3 : st & 1) * BBUF;
+          if (st + 1 < steps) stage_b(st + 1, (st + 1) & 1);
+          const char* Bl = smem + WBUF + (st & 1) * BBUF;
 #pragma unroll
           for (int j = 0; j < TN; ++j) bfr[j] = rdB(Bl, 0, j);
           __builtin_amdgcn_s_setprio(1);
@@ -230,12 +215,7 @@ __global__ __launch_bounds__(256, 2) void wconv2_kernel(const WConvDev P) {
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             stage_w(c + 1);
           }
-          // step st + 1 landed; with NB = 3 step st + 2 may stay in flight — except after a window re-stage (issued
-          // behind it: drain) and when no step st + 2 was issued
-          if (NB == 3 && st + 2 < steps && !(tap == K - 1 && c + 1 < nC))
-            asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
           if (tap == K - 1) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) af[i] = rdA(0, 0, i);
@@ -877,25 +857,14 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
     void* tok = prof_start(s);
     const dim3 grid((unsigned)nwg2), blk(256);
     const bool gl = a.geglu_plane != nullptr;
-    // 256 x 96 tiles: three weight buffers (ALCM_WCONV2_NB=2: two, the A/B reference)
-    const bool nb3 = knobs().wconv2_nb != 2;
     auto go = [&](auto bm_c) {
       constexpr int BM = decltype(bm_c)::value, BN = BM == 256 ? 96 : 192;
-      auto launch = [&](auto nb_c) {
-        constexpr int NB = decltype(nb_c)::value;
-        if (a.prec == PREC_F16) {
-          if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true, BM, BN, NB>), grid, blk, 0, s, P);
-          else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, BM, BN, NB>), grid, blk, 0, s, P);
-        } else {
-          if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true, BM, BN, NB>), grid, blk, 0, s, P);
-          else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, BM, BN, NB>), grid, blk, 0, s, P);
-        }
-      };
-      if constexpr (BM == 256) {
-        if (nb3) launch(std::integral_constant<int, 3>{});
-        else launch(std::integral_constant<int, 2>{});
+      if (a.prec == PREC_F16) {
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_F16, true, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_F16, false, BM, BN>), grid, blk, 0, s, P);
       } else {
-        launch(std::integral_constant<int, 2>{});
+        if (gl) hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, true, BM, BN>), grid, blk, 0, s, P);
+        else hipLaunchKernelGGL((wconv2_kernel<PREC_BF16, false, BM, BN>), grid, blk, 0, s, P);
       }
     };
     if (t256) {

@@ -896,39 +896,3 @@ def test_wconv3_ksplit_underfilled(K, B, acc, monkeypatch):
     e_s, e_1 = rel_l2(ys.numpy(), y1.numpy()), rel_l2(ys.numpy(), ref.numpy())
     print(f"ksplit B{B}: split vs unsplit {e_s:.2e}, vs F.conv1d {e_1:.2e}")
     assert e_s < 1e-6 and e_1 < 1e-5
-
-
-@pytest.mark.parametrize("C,N,T,k,geglu", [(384, 768, 2000, 7, False), (576, 4608, 467, 9, True)])
-def test_wconv2_tile256_three_weight_buffers(K, C, N, T, k, geglu, monkeypatch):
-    """wconv2's 256 x 96 tiles with three weight buffers (step s + 2 staged during step s, ALCM_WCONV2_NB=3, the
-    default) == two (ALCM_WCONV2_NB=2) bit for bit — the same products in the same order — and vs F.conv1d: the DiT
-    GEGLU FFN up-projection's shape (new_attention.py:48-55) and a BigVGAN-like k7 with a residual."""
-    from audiolcm_amd import _hip
-    B = 4
-    x = _r((B, T, C), 180, 0.5)
-    w, bias = _r((N, C, k), 181, 1.0 / np.sqrt(C * k)), _r((N,), 182, 0.05)
-    r = None if geglu else _r((B, T, N), 183)
-    pl = K.operand_planes(dev(x), 2)
-    pw = K.pack_conv_weight(dev(w))
-    monkeypatch.setenv("ALCM_WCONV3", "0")
-    outs = {}
-    try:
-        for nb in ("3", "2"):
-            monkeypatch.setenv("ALCM_WCONV2_NB", nb)
-            _hip.reload_knobs()
-            if geglu:
-                outs[nb] = K.opconv(pl, C, dev(w), dev(bias), 1, 2, packed=pw, geglu=True).cpu()
-            else:
-                outs[nb] = K.opconv(pl, C, dev(w), dev(bias), 1, 2, residual=dev(r), packed=pw).cpu()
-    finally:
-        monkeypatch.delenv("ALCM_WCONV3")
-        monkeypatch.delenv("ALCM_WCONV2_NB")
-        _hip.reload_knobs()
-    assert torch.equal(outs["3"], outs["2"])
-    y = F.conv1d(x.half().float().permute(0, 2, 1), w.half().float(), bias, padding=k // 2).permute(0, 2, 1)
-    if geglu:
-        ref = y[..., 0::2] * F.gelu(y[..., 1::2])
-        got = outs["3"][0].view(torch.float16).float()
-        assert rel_l2(got.numpy(), ref.numpy()) < 1e-3
-    else:
-        assert rel_l2(outs["3"].numpy(), (y + r).numpy()) < 1e-5
