@@ -124,7 +124,6 @@ struct Knobs {
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
-  int tconv_cfr = 1;             // ALCM_TCONV_CFR: resident tail conv, residual epilogues from the accumulator layout (0 = staged)
   int ksplit = 1;                // ALCM_KSPLIT: wconv3 K parts on under-filled grids where a workspace is given (0 = never)
   int xp[4] = {0, 0, 0, 0};      // ALCM_XP0..3: scratch switches for an experiment in flight (no default path reads them)
 };

@@ -36,7 +36,6 @@ static Knobs read_knobs() {
   k.xp[3] = env_int("ALCM_XP3", 0);
   k.conv1_h16 = env_int("ALCM_CONV1_H16", 1);
   k.ksplit = env_int("ALCM_KSPLIT", 1);
-  k.tconv_cfr = env_int("ALCM_TCONV_CFR", 1);
   return k;
 }
 

@@ -185,54 +185,6 @@ __device__ __forceinline__ void tc_epilogue(const f32x4 (&acc)[TM][TN], const fl
   tm.mark(5);
 }
 
-// tc_epilogue with the residual prefetched in the accumulator (C-fragment) layout, CF form: v = acc + bias + res is
-// formed in registers — the same operations in the same order as tc_epilogue's staged pass, so the results are
-// bit-identical — and the fp32 state / accumulated output stored straight from registers (4-B stores, 16 lanes of
-// consecutive columns per row); the staged tile then only feeds the Activation1d (conv2) or is not written at all (a
-// resblock's last conv2).  Saves the staged tile's read-modify-write pass; the barrier count stays the loader's.
-template <int NS, int BM, int R, int TM, int TN, int NT, bool ACT, bool OUTW, bool ACC, bool DG>
-__device__ __forceinline__ void tc_epilogue_cf(const f32x4 (&acc)[TM][TN], const float (&bias_r)[TN],
-                                             const float (&rc)[TM][TN][4], float* ot, int wr0, int t0, int e0, int E,
-                                             int b, int n0, const TConvDev& P, TcTimer<DG>& tm) {
-  constexpr int OTS = NS + 4;
-  const int lane = threadIdx.x & 63, q4 = lane >> 4, l16 = lane & 15;
-  const int e_hi = min(e0 + E, P.T);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = wr0 + i * 16 + q4 * 4 + r;
-      const int t = t0 + m;
-      const bool own = t >= e0 && t < e_hi;
-      float* const orow = P.out + ((int64_t)b * P.T + (own ? t : 0)) * P.N + n0;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = j * 16 + l16;
-        if (n >= NS) continue;
-        float v = acc[i][j][r] + bias_r[j];
-        v += rc[i][j][r];
-        if constexpr (ACT) ot[m * OTS + n] = v;
-        if constexpr (OUTW)
-          if (own && !(DG && (P.ablate & 16))) orow[n] = v;
-        if constexpr (ACC)
-          if (own && !(DG && (P.ablate & 16))) {
-            v *= P.out_scale;
-            if (P.accumulate) v += orow[n];
-            orow[n] = v;
-          }
-      }
-    }
-  __syncthreads();
-  tm.mark(3);
-  if constexpr (ACT) __syncthreads();  // (tc_epilogue's residual-pass barrier: the loader counts it)
-  tm.mark(4);
-  if constexpr (ACT) {
-    if (DG && (P.ablate & 8)) act_epilogue_ct<PREC_F16, R, NS / 2, true>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, threadIdx.x, NT);
-    else act_epilogue_ct<PREC_F16, R, NS / 2>(ot, OTS, t0, e0, e_hi, P.T, n0, b, P.act, threadIdx.x, NT);
-  }
-  tm.mark(5);
-}
-
 // one wave's LDS-DMA of a tile window through a buffer descriptor over the batch's plane rows (device-only: the
 // buffer builtins inside a kernel lambda make the host pass drop the kernel's launch stub): slot i of this lane at
 // byte offset off[i] + shift, out-of-range offsets (before row 0, past the batch, or the 0x7fffffff of an unused
@@ -282,9 +234,7 @@ static constexpr int tc_wbytes(int C, int NS, int NPB, int kmax) {
 // window as soon as the K loop is done with the current one, under the epilogue.
 // OCC workgroups per CU (the launch bound on registers; the LDS must allow it too).
 // DG: the diagnostics instantiation (ablation bits, phase trace); false in production.
-// CFR: the residual in the accumulator layout (tc_epilogue_cf) where there is one.
-template <int C, int NS, int NPB, int BM, int R, int KMAX, int OCC, bool ACT, bool RES, bool OUTW, bool ACC, bool DG,
-          bool CFR = false>
+template <int C, int NS, int NPB, int BM, int R, int KMAX, int OCC, bool ACT, bool RES, bool OUTW, bool ACC, bool DG>
 __global__ __launch_bounds__(BM * 2 + 64, OCC == 1 ? 1 : (OCC * (BM / 32 + 1) + 3) / 4) void tconv_kernel(const TConvDev P) {
   constexpr int NW = BM / 32, NT = NW * 64;             // compute waves / threads
   constexpr int TM = 2, NSP = (NS + 15) / 16 * 16, TN = NSP / 16;
@@ -397,21 +347,8 @@ __global__ __launch_bounds__(BM * 2 + 64, OCC == 1 ? 1 : (OCC * (BM / 32 + 1) + 
     const int t0 = e0 - ACT_EPI_HALO;                 // first computed row
 
     // residual rows of the tile (clamped to [0, T)) into registers, waited for in the epilogue
-    constexpr bool CF = CFR && RES;
-    float4 rv[CF ? 1 : NRES];
-    float rc[CF ? TM : 1][CF ? TN : 1][4];
-    if constexpr (CF) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = min(max(t0 + wr0 + i * 16 + q4 * 4 + r, 0), P.T - 1);
-          const float* const rrow = P.res + ((int64_t)b * P.T + t) * P.N + n0;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) rc[i][j][r] = (j * 16 + l16 < NS) ? rrow[j * 16 + l16] : 0.f;
-        }
-    }
-    if constexpr (RES && !CF) {
+    float4 rv[NRES];
+    if constexpr (RES) {
 #pragma unroll
       for (int i = 0; i < NRES; ++i) {
         const int e = tid + i * NT;
@@ -486,8 +423,7 @@ __global__ __launch_bounds__(BM * 2 + 64, OCC == 1 ? 1 : (OCC * (BM / 32 + 1) + 
       continue;
     }
 
-    if constexpr (CF) tc_epilogue_cf<NS, BM, R, TM, TN, NT, ACT, OUTW, ACC, DG>(acc, bias_r, rc, ot, wr0, t0, e0, E, b, n0, P, tm);
-    else tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, DG>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
+    tc_epilogue<NS, BM, R, TM, TN, NT, NRES, ACT, RES, OUTW, ACC, DG>(acc, bias_r, rv, ot, wr0, t0, e0, E, b, n0, P, tm);
     __syncthreads();  // C: staged-tile reads retired
     tm.mark(6);
     tm.tile();
@@ -698,15 +634,8 @@ bool tconv_supported(int prec, int C, int N, int ksize, int dil) {
 template <int C, int NS, int NPB, int BM, int R, int KMAX, int OCC, bool ACT, bool RES, bool OUTW, bool ACC>
 static void tc_launch(const TConvDev& P, bool diag, int grid, hipStream_t s) {
   const dim3 g(grid), blk(BM * 2 + 64);
-  // the residual in the accumulator layout (ALCM_TCONV_CFR, default on) for the residual epilogues
-  const bool cf = RES && knobs().tconv_cfr != 0;
-  if (diag) {
-    if (cf) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, true, RES>), g, blk, 0, s, P);
-    else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, true>), g, blk, 0, s, P);
-  } else {
-    if (cf) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, false, RES>), g, blk, 0, s, P);
-    else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, false>), g, blk, 0, s, P);
-  }
+  if (diag) hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, true>), g, blk, 0, s, P);
+  else hipLaunchKernelGGL((tconv_kernel<C, NS, NPB, BM, R, KMAX, OCC, ACT, RES, OUTW, ACC, false>), g, blk, 0, s, P);
 }
 
 template <int C, int NS, int NPB, int BM, int R, int KMAX = 11, int OCC = 1>

@@ -21,6 +21,8 @@ def short(name):
 
 def counters(path, counter, scale=1024.0):
     per = collections.defaultdict(list)
+    if not os.path.exists(path):  # scripts/pmc_compact.py output (per-dispatch sums) in its place
+        path = os.path.join(os.path.dirname(path), "compact.csv")
     if not os.path.exists(path):
         return per
     for r in csv.DictReader(open(path)):
