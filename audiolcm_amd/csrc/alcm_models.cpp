@@ -1679,6 +1679,8 @@ struct TextWs {
   float *x, *tmp, *qkv, *S, *O, *inter, *e1, *g, *mean, *rstd;
   float* wi;  // T5 wi GEMM output before the gated GELU (plane path)
   u16* pl;    // operand plane of the linears' A (plane path)
+  float* kp;  // K-split partial sums of the under-filled linears (alcm_opconv_args.ksplit_ws)
+  int64_t kp_floats;
 };
 static TextWs plan_text(const TextW& X, Bump& bp, int B, int L) {
   const size_t R = (size_t)B * L;
@@ -1698,6 +1700,8 @@ static TextWs plan_text(const TextW& X, Bump& bp, int B, int L) {
   w.rstd = bp.take<float>(R);
   w.wi = bp.take<float>(R * 2 * (size_t)X.t_ff);
   w.pl = bp.take<u16>(R * (size_t)std::max({X.b_inter, 2 * X.t_ff, (int)dmax, (int)inner}));
+  w.kp_floats = (int64_t)8 * R * (int64_t)dmax;  // up to 8 parts of an R x dmax output
+  w.kp = bp.take<float>((size_t)w.kp_floats);
   return w;
 }
 
@@ -1745,7 +1749,8 @@ static int lin(hipStream_t s, int prec, int R, const float* x, int C, const Conv
 // the same linear on an F16 / BF16 operand plane (alcm_opconv, k = 1: the wide-layer / plane conv kernels): y (R, N) =
 // plane (R, C) W^T (+ bias) (+ res) with out_act; the plane is written by the caller
 static int plane_lin(hipStream_t s, int prec, int R, const u16* plane, int C, const ConvW& w, float* y,
-                     const float* res, int act, int64_t plane_lo = 0, void* out_plane = nullptr) {
+                     const float* res, int act, int64_t plane_lo = 0, void* out_plane = nullptr,
+                     float* kws = nullptr, int64_t kws_floats = 0) {
   if (w.w.cpad != C || w.w.taps != 1) return set_error(ALCM_E_INVALID, "plane_lin: plane width != packed Cin");
   alcm_opconv_args g;
   std::memset(&g, 0, sizeof(g));
@@ -1753,6 +1758,7 @@ static int plane_lin(hipStream_t s, int prec, int R, const u16* plane, int C, co
   g.w = w.w.p; g.w_lo_off = w.w.lo; g.kpad = w.w.kpad; g.N = w.w.rows;
   g.bias = w.b; g.res = res; g.out = y; g.out_act = act; g.out_scale = 1.f; g.prec = prec;
   g.out_plane = out_plane;  // (then y == nullptr: the result as a PREC plane)
+  g.ksplit_ws = kws; g.ksplit_ws_floats = kws_floats;  // K parts where the grid under-fills the chip (alcm_wconv.hip)
   return opconv(g, s);
 }
 
@@ -1788,12 +1794,12 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
         ALCM_TRY(mha(s, pl, B, L, X.b_heads, bdh, w.qkv, 1.0f / sqrtf((float)bdh), nullptr, 0, w.S, w.O));
         ALCM_TRY(to_planes(w.O, w.pl, R, H, H, pl, s));
       }
-      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.ao, w.tmp, w.x, 0));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.ao, w.tmp, w.x, 0, 0, nullptr, w.kp, w.kp_floats));
       ALCM_TRY(layer_norm_plane(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, w.pl, pl, s));
       ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln1.g, Ly.ln1.b, nullptr, 0, w.x, H, s));
       ALCM_TRY(plane_lin(s, pl, R, w.pl, H, Ly.inter, w.inter, nullptr, ACT_GELU_ERF));
       ALCM_TRY(to_planes(w.inter, w.pl, R, X.b_inter, X.b_inter, pl, s));
-      ALCM_TRY(plane_lin(s, pl, R, w.pl, X.b_inter, Ly.out, w.tmp, w.x, 0));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, X.b_inter, Ly.out, w.tmp, w.x, 0, 0, nullptr, w.kp, w.kp_floats));
       ALCM_TRY(layer_norm(w.tmp, R, H, H, X.b_eps, Ly.ln2.g, Ly.ln2.b, nullptr, 0, w.x, H, s));
       continue;
     }
@@ -1838,7 +1844,7 @@ static int text_encode(alcm_model* m, const int64_t* clap_ids, const int64_t* t5
         ALCM_TRY(mha(s, pl, B, L, X.t_heads, X.t_dkv, w.qkv, 1.0f, X.t_bias, X.max_len, w.S, w.O));
         ALCM_TRY(to_planes(w.O, w.pl, R, TI, TI, pl, s));
       }
-      ALCM_TRY(plane_lin(s, pl, R, w.pl, TI, Bk.o, w.x, w.x, 0));
+      ALCM_TRY(plane_lin(s, pl, R, w.pl, TI, Bk.o, w.x, w.x, 0, 0, nullptr, w.kp, w.kp_floats));
       ALCM_TRY(rms_norm_plane(w.x, R, D, X.t_eps, Bk.ln1, w.pl, pl, s));
       ALCM_TRY(plane_lin(s, pl, R, w.pl, D, Bk.wi, w.wi, nullptr, 0));
       if (ps == PREC_SPLIT) {

@@ -896,3 +896,32 @@ def test_wconv3_ksplit_underfilled(K, B, acc, monkeypatch):
     e_s, e_1 = rel_l2(ys.numpy(), y1.numpy()), rel_l2(ys.numpy(), ref.numpy())
     print(f"ksplit B{B}: split vs unsplit {e_s:.2e}, vs F.conv1d {e_1:.2e}")
     assert e_s < 1e-6 and e_1 < 1e-5
+
+
+@pytest.mark.parametrize("C,N", [(1024, 1024), (3072, 768), (768, 768)])
+def test_wconv2_ksplit_text_linears(K, C, N):
+    """K-split two-workgroup wide conv on the text towers' under-filled linears (2464 rows = 32 prompts x 77 tokens:
+    the T5 attention out-projection 1024 -> 1024 with its ragged last N tile, the BERT output 3072 -> 768 and
+    attention output 768 -> 768, each + bias + residual; modules.py:567-582 via HF T5 / BERT): vs the unsplit launch
+    (summation order only) and vs F.linear on the fp16 operands, bit-stable."""
+    from audiolcm_amd import _hip
+    R = 2464
+    x = _r((1, R, C), 190, 0.5)
+    w, bias = _r((N, C, 1), 191, 1.0 / np.sqrt(C)), _r((N,), 192, 0.05)
+    r = _r((1, R, N), 193)
+    pl = K.operand_planes(dev(x), 2)
+    pw = K.pack_conv_weight(dev(w))
+    ws = torch.empty(8 * R * N, device="cuda")
+    run = lambda split: K.opconv(pl, C, dev(w), dev(bias), 1, 2, residual=dev(r), packed=pw,
+                                 ksplit_ws=ws if split else None).cpu()
+    _hip.profile_begin()
+    ys = run(True)
+    torch.cuda.synchronize()
+    names = [p["name"] for p in _hip.profile_end()]
+    assert any("wconv2_kernel" in n and "ksplit_reduce" in n for n in names), names
+    y1 = run(False)
+    assert torch.equal(ys, run(True))
+    ref = F.linear(x.half().float()[0], w.half().float()[..., 0], bias) + r[0]
+    e_s, e_r = rel_l2(ys.numpy(), y1.numpy()), rel_l2(ys[0].numpy(), ref.numpy())
+    print(f"wconv2 ksplit C{C} N{N}: split vs unsplit {e_s:.2e}, vs F.linear {e_r:.2e}")
+    assert e_s < 1e-6 and e_r < 1e-5
