@@ -1483,8 +1483,10 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // go to opconv_kernel, whose K order differs): the A/B stays bit-exact at every size
     const bool h16 = knobs().conv1_h16 && pamp == PREC_F16 && act_mfma_ok(S.cout, round_up(S.cout, 32), pamp) &&
                      (int64_t)B * To >= 1024;
-    // the three chains' first Activation1d in one pass over u (their own planes, same taps)
-    bool act3 = conc && fuse && S.rb.size() == 3 &&
+    // the three chains' first Activation1d in one pass over u (their own planes, same taps) — with the chains on
+    // their streams and serialised alike (each chain on its own buffers then), so the serialised profile pass runs
+    // the same kernels as the concurrent one
+    bool act3 = fuse && S.rb.size() == 3 &&
                 !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
     for (size_t j = 1; act3 && j < S.rb.size(); ++j)
       act3 = !std::memcmp(S.rb[j].act[0].fup, S.rb[0].act[0].fup, sizeof(S.rb[0].act[0].fup)) &&
@@ -1502,7 +1504,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     }
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
-      const VocChain& cb = w.ch[conc ? j : 0];
+      const VocChain& cb = w.ch[(conc || act3) ? j : 0];
       const hipStream_t sj = (conc && j > 0) ? ax->s[j - 1] : s;
       const float* cur = u;
       float* nxt = cb.rb;
