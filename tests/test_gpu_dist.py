@@ -25,7 +25,10 @@ ARGS = ["--steps", "1", "--warmup", "0", "--also-other-mode", "0", "--cpu-baseli
 
 
 def _run(cmd, tmp_path, name):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=REPO)
+    # ALCM_KSPLIT=0: the K split is chosen by how full a layer's grid is, so 64 prompts in one process and 32 per rank
+    # would sum the DiT FFN down-projection in different orders (same parity, DESIGN.md §2 "Sensitivity"); with it off
+    # both batch sizes run the same kernel variants and the gathered waveforms must match bit for bit
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=REPO, ALCM_KSPLIT="0")
     with open(tmp_path / f"{name}.log", "w") as log:
         r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=log, text=True, timeout=420, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + open(tmp_path / f"{name}.log").read()[-4000:]
