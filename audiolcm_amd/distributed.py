@@ -65,6 +65,25 @@ def all_reduce_max(value: float, group=None) -> float:
     return float(t.item())
 
 
+def all_gather_rows_async(local: torch.Tensor, n_total: int, group=None):
+    """all_gather_rows without waiting: -> (out, work).  Over RCCL (equal shards, device tensors) the gather is
+    enqueued on the collective's own stream behind the producer of ``local`` and ``work.wait()`` orders the caller's
+    current stream after it, so the next batch's kernels overlap the waveform exchange (bench.py keeps one gather in
+    flight).  Other cases (gloo, ragged shards, no process group) complete before returning, with work = None."""
+    if not dist.is_initialized():
+        return local, None
+    world = dist.get_world_size(group)
+    if not local.is_cuda or dist.get_backend(group) != "nccl" or n_total % world:
+        return all_gather_rows(local, n_total, group), None
+    lo, hi = shard_range(n_total, dist.get_rank(group), world)
+    if local.shape[0] != hi - lo:
+        raise ValueError(f"all_gather_rows_async: local shard has {local.shape[0]} rows, expected {hi - lo}")
+    src = local.contiguous()
+    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    work = dist.all_gather_into_tensor(out, src, group=group, async_op=True)
+    return out, work
+
+
 def all_gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """Gather per-rank row blocks (contiguous shards of n_total rows) into the full (n_total, ...) tensor.
 

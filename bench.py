@@ -354,7 +354,7 @@ def main():
     if spawn:
         sys.exit(spawn_ranks(spawn, sys.argv[1:]))
     from audiolcm_amd import _hip, recipe
-    from audiolcm_amd.distributed import all_gather_rows, all_reduce_max, barrier, init_from_env
+    from audiolcm_amd.distributed import all_gather_rows_async, all_reduce_max, barrier, init_from_env
     from audiolcm_amd.pipeline import AudioLCMPipeline
     import torch.distributed as dist
 
@@ -372,15 +372,28 @@ def main():
     clip_sec = T * 2 * HOP / SR
 
     gathered = {}
+    inflight = []  # the previous step's waveform all-gather (RCCL, async): overlaps this step's kernels
+
+    def settle():
+        while inflight:
+            w = inflight.pop()
+            if w is not None:
+                w.wait()
 
     def step():
         out = pipe.generate(cond, seeds=ids, steps=S, latent_len=T)
-        gathered["wav"] = all_gather_rows(out["wav"], B * world) if coll else out["wav"]
+        settle()  # at most one gather in flight
+        if coll:
+            gathered["wav"], work = all_gather_rows_async(out["wav"], B * world)
+            inflight.append(work)
+        else:
+            gathered["wav"] = out["wav"]
         return out
 
     def timed(k, profile):
         for _ in range(a.warmup):
             step()
+        settle()
         torch.cuda.synchronize()
         if coll:
             barrier()
@@ -390,6 +403,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(k):
             step()
+        settle()  # the last gather is inside the timed region
         torch.cuda.synchronize()
         if coll:
             barrier()

@@ -2,7 +2,8 @@
 import torch
 import torch.distributed as dist
 
-from audiolcm_amd.distributed import all_reduce_max, barrier, generate_sharded, init_from_env, shard_range
+from audiolcm_amd.distributed import (all_gather_rows_async, all_reduce_max, barrier, generate_sharded, init_from_env,
+                                      shard_range)
 
 
 def main():
@@ -19,6 +20,10 @@ def main():
     lo, hi = shard_range(n, rank, world)
     assert hi - lo == (3 if rank == 0 else 2)
     assert all_reduce_max(0.5 + rank) == 0.5 + world - 1  # bench.py's max-over-ranks timing
+    # bench.py's gather entry (async over RCCL; over gloo it completes before returning)
+    lo, hi = shard_range(n, rank, world)
+    full2, work = all_gather_rows_async(expect[lo:hi], n)
+    assert work is None and torch.equal(full2, expect)
     barrier()
     if rank == 0:
         print("GATHER_OK")
