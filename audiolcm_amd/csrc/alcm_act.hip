@@ -80,6 +80,27 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
   const int j0 = t0 + run * 8;
   const int jn = min(8, T - j0);
 
+  // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer order compiles
+  // to 6-deep dependent chains with a wait state between links)
+  auto up_fir = [&](f32x2 (&u)[AC_SEG]) {
+#pragma unroll
+    for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+      for (int q = 0; q < AC_SEG; ++q) {
+        const int ku = 2 * kk + ((q & 1) ? 0 : 1);
+        u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
+      }
+  };
+  // NSET = 3 (the three resblocks' first Activation1d of a tail stage): UpSample1d does not depend on the SnakeBeta
+  // parameters, so the samples are computed once for the three sets (x3 launches 1.49 -> 1.37 ms/step, bit-identical,
+  // profiles/r6j); with one set the FIR stays inside the set's phase 1, where it fills the SnakeBeta / LDS latency
+  // (hoisted there: +5.6 %, profiles/r6f)
+  f32x2 u3[NSET > 1 ? AC_SEG : 1];
+  if constexpr (NSET > 1)
+    if (live && interior) up_fir(u3);
+
 #pragma unroll
   for (int st = 0; st < NSET; ++st) {
     const f32x2 ear = live ? f32x2{S.aexp[st][c], S.aexp[st][c + 1]} * INV_PI : f32x2{0.f, 0.f};
@@ -88,20 +109,15 @@ __global__ __launch_bounds__(256) void act_coop_kernel(const float* __restrict__
     //      x-window offsets are compile-time); replicate padding = the sample at the clamped index
     if (live) {
       if (interior) {
-        // tap-outer order: the 18 accumulation chains are independent instructions back to back (a q-outer
-        // order compiles to 6-deep dependent chains with a wait state between links)
-        f32x2 u[AC_SEG];
+        if constexpr (NSET > 1) {
 #pragma unroll
-        for (int q = 0; q < AC_SEG; ++q) u[q] = f32x2{0.f, 0.f};
+          for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u3[q], ear, h);
+        } else {
+          f32x2 u[AC_SEG];
+          up_fir(u);
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk)
-#pragma unroll
-          for (int q = 0; q < AC_SEG; ++q) {
-            const int ku = 2 * kk + ((q & 1) ? 0 : 1);
-            u[q] = fma2(f32x2{f.up[ku], f.up[ku]}, win[(q + 5 - ku) / 2 + 3], u[q]);
-          }
-#pragma unroll
-        for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
+          for (int q = 0; q < AC_SEG; ++q) sv[(seg * AC_SEG + q) * AC_RS + p] = snake2(u[q], ear, h);
+        }
       } else {
         for (int q = 0; q < AC_SEG; ++q) {
           int m = mb + q;
