@@ -428,6 +428,172 @@ __global__ __launch_bounds__(256, (AmGeo<TT>::OCC)) void act_mfma_kernel(const v
   if (DEFER && ntile > 0) store_tile((tile0 + ntile - 1) * AM_TT);
 }
 
+// act_mfma_kernel for the three resblocks' first Activation1d of a wide stage (one input, three SnakeBeta parameter
+// sets, the same FIR taps): x staged and the up products computed ONCE per tile and kept as fp32 fragments (UPB x 4
+// registers), then per set SnakeBeta -> (s, s) pairs -> down products -> that set's plane, the staged output tile
+// stored right away (no one-tile deferral: three tiles would be in flight).  The same operations per set as
+// act_mfma_kernel<TT, .., false>: bit-identical to three calls.
+template <int TT>
+__global__ __launch_bounds__(256, 2) void act_mfma3_kernel(const float* __restrict__ xin, const ActSets S, int T, int C,
+                                                           int Cp, const Taps12O f, int strips_t, int tiles_c) {
+  constexpr float INV_PI = 0.318309886183790671538f;
+  constexpr int AM_TT = TT, AM_XR = AmGeo<TT>::XR, AM_UPB = AmGeo<TT>::UPB;
+  constexpr int XWS = 16 * AM_XS + 4;
+  __shared__ __attribute__((aligned(16))) uint32_t xs[4 * XWS];
+  constexpr int OS = 72;
+  __shared__ __attribute__((aligned(16))) u16 ob[AM_TT * OS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q4 = lane >> 4, l16 = lane & 15;
+  int bid = blockIdx.x;
+  const int ct = bid % tiles_c;
+  bid /= tiles_c;
+  const int st = bid % strips_t;
+  const int b = bid / strips_t;
+  const int c0 = ct * 64 + wave * 16;
+  const int tile0 = st * AM_STRIP, ntile = min(AM_STRIP, (T + AM_TT - 1) / AM_TT - tile0);
+  uint32_t* const xw = xs + wave * XWS;
+  f16x8 aup, bdn[3];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int rr = 4 * q4 + e / 2;
+    const int ku = l16 - 2 * rr + 10;
+    const float tv = (ku >= 0 && ku < 12) ? am_sel12(f.up, ku) : 0.f;
+    const _Float16 hi = (_Float16)tv;
+    aup[e] = (e & 1) ? (_Float16)(tv - (float)hi) : hi;
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 16 * p + 4 * q4 + e / 2 - 2 * l16;
+      const float tv = (k >= 0 && k < 12) ? am_sel12(f.dn, k) : 0.f;
+      const _Float16 hi = (_Float16)tv;
+      bdn[p][e] = (e & 1) ? (_Float16)(tv - (float)hi) : hi;
+    }
+  const int cl = c0 + l16;
+  float ear[3], hh[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    ear[k] = S.aexp[k][cl] * INV_PI;
+    hh[k] = S.ibeta[k][cl] * 0.5f;
+  }
+  const char* const xb = reinterpret_cast<const char*>(xin) + ((int64_t)b * T * C + ct * 64 + (lane & 15) * 4) * 4;
+  float4 xv[AM_XR / 16];
+  auto xrow = [&](int it) { return it * 16 + wave * 4 + (lane >> 4); };
+  auto load_x = [&](int t0) {
+#pragma unroll
+    for (int it = 0; it < AM_XR / 16; ++it) {
+      const int t = min(max(t0 - 5 + xrow(it), 0), T - 1);
+      xv[it] = *reinterpret_cast<const float4*>(xb + (int64_t)t * C * 4);
+    }
+  };
+  load_x(tile0 * AM_TT);
+  for (int tl = 0; tl < ntile; ++tl) {
+    const int t0 = (tile0 + tl) * AM_TT;
+    {
+      uint32_t* const xo = xs + ((lane & 15) >> 2) * XWS;
+      const int c = (lane & 3) * 4;
+#pragma unroll
+      for (int it = 0; it < AM_XR / 16; ++it) {
+        const int r = xrow(it);
+        xo[(c + 0) * AM_XS + r] = am_pair(xv[it].x);
+        xo[(c + 1) * AM_XS + r] = am_pair(xv[it].y);
+        xo[(c + 2) * AM_XS + r] = am_pair(xv[it].z);
+        xo[(c + 3) * AM_XS + r] = am_pair(xv[it].w);
+      }
+    }
+    if (tl + 1 < ntile) load_x(t0 + AM_TT);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // the up products of the tile, once for the three sets
+    f32x4 ub[AM_UPB];
+#pragma unroll
+    for (int bk = 0; bk < AM_UPB; ++bk) {
+      const f16x8 bx = *reinterpret_cast<const f16x8*>(xw + l16 * AM_XS + 8 * bk + 4 * q4);
+      ub[bk] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aup, bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    const int i_lo = 5 - 2 * t0, i_hi = 2 * T + 4 - 2 * t0;
+#pragma unroll
+    for (int set = 0; set < 3; ++set) {
+      uint4 sf[AM_UPB];
+#pragma unroll
+      for (int bk = 0; bk < AM_UPB; ++bk) {
+        uint32_t* op = reinterpret_cast<uint32_t*>(&sf[bk]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sv = fmaf(-hh[set], __builtin_amdgcn_cosf(ub[bk][r] * ear[set]), ub[bk][r] + hh[set]);
+          op[r] = am_pair(sv);
+        }
+      }
+      if (i_lo > 0 || i_hi < AM_UPB * 16 - 1) {  // DownSample1d replicate padding (act_mfma_kernel)
+        auto pick = [&](int i) -> uint32_t {
+          uint32_t v = 0u;
+#pragma unroll
+          for (int bk = 0; bk < AM_UPB; ++bk) {
+            const uint32_t* sp = reinterpret_cast<const uint32_t*>(&sf[bk]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v = (bk == (i >> 4) && r == (i & 3)) ? sp[r] : v;
+          }
+          return v;
+        };
+        const int il = max(i_lo, 0), ih = min(max(i_hi, 0), AM_UPB * 16 - 1);
+        const uint32_t vlo = (uint32_t)__shfl((int)pick(il), ((il >> 2) & 3) * 16 + l16);
+        const uint32_t vhi = (uint32_t)__shfl((int)pick(ih), ((ih >> 2) & 3) * 16 + l16);
+#pragma unroll
+        for (int bk = 0; bk < AM_UPB; ++bk) {
+          uint32_t* sp = reinterpret_cast<uint32_t*>(&sf[bk]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * bk + 4 * q4 + r;
+            if (i_lo > 0 && i < i_lo) sp[r] = vlo;
+            if (i_hi >= 0 && i_hi < AM_UPB * 16 - 1 && i > i_hi) sp[r] = vhi;
+          }
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < AM_TT / 16; ++d) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, sf[2 * d + p]), bdn[p], acc, 0, 0, 0);
+        uint2 w;
+        w.x = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[0]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[1]) << 16);
+        w.y = (uint32_t)__builtin_bit_cast(u16, (_Float16)acc[2]) | ((uint32_t)__builtin_bit_cast(u16, (_Float16)acc[3]) << 16);
+        *reinterpret_cast<uint2*>(ob + (16 * d + l16) * OS + wave * 16 + 4 * q4) = w;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the set's tile staged
+      u16* const yb = S.y[set] + (int64_t)b * T * Cp + ct * 64;
+#pragma unroll
+      for (int k = 0; k < AM_TT * 8 / 256; ++k) {
+        const int e = tid + 256 * k, r = e >> 3, sg = e & 7;
+        if (t0 + r < T)
+          *reinterpret_cast<uint4*>(yb + (int64_t)(t0 + r) * Cp + sg * 8) = *reinterpret_cast<const uint4*>(ob + r * OS + sg * 8);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // ob reads retired (and, after the last set,
+                                                                        // every wave past its up reads of xs)
+    }
+  }
+}
+
+int act_mfma3(const float* x, void* const y[3], int B, int T, int C, int Cp, const float* const alpha_exp[3],
+              const float* const inv_beta[3], const Taps12O& f, hipStream_t s) {
+  if ((((uintptr_t)x) & 15)) return set_error(ALCM_E_INVALID, "act_mfma3: alignment");
+  ActSets S{};
+  for (int i = 0; i < 3; ++i) {
+    if ((((uintptr_t)y[i]) & 15)) return set_error(ALCM_E_INVALID, "act_mfma3: alignment");
+    S.y[i] = (u16*)y[i];
+    S.aexp[i] = alpha_exp[i];
+    S.ibeta[i] = inv_beta[i];
+  }
+  constexpr int TT = 64;
+  const int tiles_t = (T + TT - 1) / TT, tiles_c = C / 64;
+  const int strips_t = (tiles_t + AM_STRIP - 1) / AM_STRIP;
+  const int64_t nwg = (int64_t)B * strips_t * tiles_c;
+  if (nwg >= (1ll << 31) || (int64_t)T * C >= (1ll << 31)) return set_error(ALCM_E_INVALID, "act_mfma3: too large");
+  hipLaunchKernelGGL(act_mfma3_kernel<TT>, dim3((unsigned)nwg), dim3(256), 0, s, x, S, T, C, Cp, f, strips_t, tiles_c);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 bool act_mfma_ok(int C, int Cp, int prec) {
   return knobs().act_mfma && prec == PREC_F16 && C >= 192 && C % 64 == 0 && Cp == C;
 }

@@ -60,6 +60,8 @@ int activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const 
 // Activation1d with both FIRs on MFMA, fp16 planes out (alcm_act.hip; C >= 192, C % 64 == 0, PREC_F16, Cp == C)
 bool act_mfma_ok(int C, int Cp, int prec);
 // x16: x is an fp16 plane [B][T][C] (the wide-stage conv1 output, alcm_opconv's out_plane) instead of fp32
+int act_mfma3(const float* x, void* const y[3], int B, int T, int C, int Cp, const float* const alpha_exp[3],
+              const float* const inv_beta[3], const Taps12O& f, hipStream_t s);
 int act_mfma(const void* x, bool x16, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
              const float* inv_beta, const Taps12O& f, hipStream_t s);
 // Activation1d of an fp16 plane x16 [B][T][C] into fp16 planes (act_mfma shapes only; ALCM_E_INVALID otherwise)
@@ -124,6 +126,7 @@ struct Knobs {
                                  // prefetch (0 = at the end of the tile)
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
+  int act_x3_mfma = 1;           // ALCM_ACT_X3_MFMA: the wide stages' three first Activation1d in one MFMA-FIR pass (0 = three)
   int ksplit = 1;                // ALCM_KSPLIT: wconv3 K parts on under-filled grids where a workspace is given (0 = never)
   int xp[4] = {0, 0, 0, 0};      // ALCM_XP0..3: scratch switches for an experiment in flight (no default path reads them)
 };

@@ -1486,8 +1486,9 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     // the three chains' first Activation1d in one pass over u (their own planes, same taps) — with the chains on
     // their streams and serialised alike (each chain on its own buffers then), so the serialised profile pass runs
     // the same kernels as the concurrent one
-    bool act3 = fuse && S.rb.size() == 3 &&
-                !act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
+    // (the narrow fused stages: the VALU kernel; the wide MFMA-FIR stages: its three-set form, ALCM_ACT_X3_MFMA)
+    const bool amok = act_mfma_ok(S.cout, round_up(S.cout, 32), pamp);
+    bool act3 = S.rb.size() == 3 && (fuse ? !amok : (amok && knobs().act_x3_mfma));
     for (size_t j = 1; act3 && j < S.rb.size(); ++j)
       act3 = !std::memcmp(S.rb[j].act[0].fup, S.rb[0].act[0].fup, sizeof(S.rb[0].act[0].fup)) &&
              !std::memcmp(S.rb[j].act[0].fdn, S.rb[0].act[0].fdn, sizeof(S.rb[0].act[0].fdn));
@@ -1526,7 +1527,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
             nxt = nxt == cb.rb ? cb.t : cb.rb;
           }
         } else {
-          ALCM_TRY(act_planes(sj, A.act[2 * l], cur, w, B, To, S.cout, pamp, cb.pl));
+          if (!(l == 0 && act3)) ALCM_TRY(act_planes(sj, A.act[2 * l], cur, w, B, To, S.cout, pamp, cb.pl));
           if (h16) {
             // conv1's only consumer is the next Activation1d, whose MFMA kernel rounds its input to fp16: conv1 writes
             // that fp16 plane (into the fp32 scratch cb.t) and the activation reads it, bit-identical at half the bytes

@@ -44,10 +44,15 @@ int activation1d_x3(const float* x, void* const y[3], int B, int T, int C, int C
     f.dn[k] = down_filter[k];
   }
   void* tok = prof_start(s);
-  ALCM_TRY(act_coop(x, y, 3, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
+  // the wide stages' MFMA FIR kernel where it applies (its fp16 FIR inputs: the mixed policy's stages 0-2)
+  const bool am = knobs().act_x3_mfma && act_mfma_ok(C, Cp, prec) && !(((uintptr_t)x) & 15) &&
+                  !(((uintptr_t)y[0]) & 15) && !(((uintptr_t)y[1]) & 15) && !(((uintptr_t)y[2]) & 15);
+  if (am) ALCM_TRY(act_mfma3(x, y, B, T, C, Cp, alpha_exp, inv_beta, f, s));
+  else ALCM_TRY(act_coop(x, y, 3, B, T, C, Cp, alpha_exp, inv_beta, f, prec, s));
   if (tok) {
     char name[64];
-    std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>, x3", prec == PREC_F16W2 ? PREC_F16 : prec);
+    if (am) std::snprintf(name, sizeof(name), "alcm::act_mfma3_kernel<64>");
+    else std::snprintf(name, sizeof(name), "alcm::act_coop_kernel<%d>, x3", prec == PREC_F16W2 ? PREC_F16 : prec);
     const double e = (double)B * T;
     prof_stop(tok, s, name, 3 * 2.0 * 36.0 * e * C, e * (4.0 * C + 3 * 2.0 * Cp * (prec == PREC_SPLIT ? 2 : 1)));
   }
