@@ -61,12 +61,52 @@ __global__ __launch_bounds__(256) void gn_affine_kernel(const float* __restrict_
   }
 }
 
+// the same statistics read as float4 pieces (C / groups % 4 == 0, 16-B aligned rows): a quarter of the load
+// instructions and index divisions; the fp64 sums see the same values in another order (53-bit accumulation of the
+// fp32 inputs: the fp32 mean / rstd it rounds to are unaffected in practice)
+__global__ __launch_bounds__(256) void gn_affine4_kernel(const float* __restrict__ x, int T, int C, int64_t sb,
+                                                         int64_t st, int groups, float eps,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* scale, float* shift,
+                                                         FastDiv cg4div) {
+  __shared__ double sh[4];
+  const int g = blockIdx.x, b = blockIdx.y;
+  const int cg = C / groups;
+  const float* base = x + (int64_t)b * sb + g * cg;
+  const int64_t n4 = (int64_t)(cg / 4) * T;
+  double s = 0.0, q = 0.0;
+  for (int64_t e = threadIdx.x; e < n4; e += 256) {
+    uint32_t t, c4;
+    cg4div.divmod((uint32_t)e, t, c4);
+    const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)t * st + 4 * c4);
+    const double a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
+    s += (a0 + a1) + (a2 + a3);
+    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+  const double n = (double)cg * T;
+  const double mean = block_sum(s, sh) / n;
+  const double var = fmax(block_sum(q, sh) / n - mean * mean, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float fmean = (float)mean;
+  for (int c = threadIdx.x; c < cg; c += 256) {
+    const int ch = g * cg + c;
+    const float sc = rstd * gamma[ch];
+    scale[(int64_t)b * C + ch] = sc;
+    shift[(int64_t)b * C + ch] = beta[ch] - fmean * sc;
+  }
+}
+
 int group_norm_affine(const float* x, int B, int T, int C, int64_t sb, int64_t st, int groups, float eps,
                       const float* gamma, const float* beta, float* scale, float* shift, hipStream_t s) {
   if (!x || !gamma || !beta || !scale || !shift || B <= 0 || T <= 0 || groups <= 0 || C % groups)
     return set_error(ALCM_E_INVALID, "group_norm_affine: bad arguments");
-  hipLaunchKernelGGL(gn_affine_kernel, dim3(groups, B), dim3(256), 0, s, x, T, C, sb, st, groups, eps, gamma, beta,
-                     scale, shift, FastDiv((uint32_t)(C / groups)));
+  const int cg = C / groups;
+  if (cg % 4 == 0 && st % 4 == 0 && sb % 4 == 0 && !(((uintptr_t)x) & 15))
+    hipLaunchKernelGGL(gn_affine4_kernel, dim3(groups, B), dim3(256), 0, s, x, T, C, sb, st, groups, eps, gamma, beta,
+                       scale, shift, FastDiv((uint32_t)(cg / 4)));
+  else
+    hipLaunchKernelGGL(gn_affine_kernel, dim3(groups, B), dim3(256), 0, s, x, T, C, sb, st, groups, eps, gamma, beta,
+                       scale, shift, FastDiv((uint32_t)cg));
   ALCM_HIP(hipGetLastError());
   return 0;
 }
