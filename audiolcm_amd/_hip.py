@@ -82,6 +82,7 @@ _SIGS = [
     ("alcm_activation1d_op", C.c_int, [fp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_activation1d_op_f16in", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, fp, fp, fp, fp, C.c_int, vp]),
     ("alcm_opconv", C.c_int, [C.POINTER(OpConvArgs), vp]),
+    ("alcm_opconv_sum", C.c_int, [C.POINTER(OpConvArgs), C.c_int, vp]),
     ("alcm_opconv_dense", C.c_int, [C.POINTER(OpConvArgs), vp]),
     ("alcm_flash_attention", C.c_int, [fp, fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
     ("alcm_layer_norm_plane", C.c_int, [fp, C.c_int, C.c_int, i64, C.c_float, fp, fp, vp, C.c_int, vp]),

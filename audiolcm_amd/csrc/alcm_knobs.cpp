@@ -37,6 +37,7 @@ static Knobs read_knobs() {
   k.conv1_h16 = env_int("ALCM_CONV1_H16", 1);
   k.ksplit = env_int("ALCM_KSPLIT", 1);
   k.act_x3_mfma = env_int("ALCM_ACT_X3_MFMA", 1);
+  k.wconv_sum = env_int("ALCM_WCONV_SUM", 1);
   return k;
 }
 

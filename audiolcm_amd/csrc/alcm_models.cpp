@@ -1355,6 +1355,20 @@ static bool stage_tconv(const StageW& S, int prec) {
   return true;
 }
 
+// the alcm_opconv arguments of a same-length conv of the planes `in` (default: the workspace planes)
+static alcm_opconv_args plane_args(const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res, float* out,
+                                   float out_scale, int accumulate, int out_act, int prec, const u16* in) {
+  alcm_opconv_args g;
+  std::memset(&g, 0, sizeof(g));
+  g.a = in ? in : w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
+  g.B = B; g.T = T; g.C = cw.w.cin; g.Cp = cw.w.cpad;
+  g.ksize = cw.w.taps; g.dil = dil; g.pad = (cw.w.taps - 1) * dil / 2;
+  g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
+  g.bias = cw.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate;
+  g.out_scale = out_scale; g.prec = prec;
+  return g;
+}
+
 static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int T, int dil, const float* res,
                       float* out, float out_scale, int accumulate, int out_act, int prec, const u16* in = nullptr,
                       const ActW* act = nullptr, u16* act_out = nullptr, bool dense = false,
@@ -1386,7 +1400,7 @@ static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int
                          (act ? M * g.N * 2.0 : 0.0);
     return tconv(g, cw.dw.p + 2 * cw.dw.lo, cw.dw.lo, cw.dw.kpad, act ? &E : nullptr, flops, bytes, s);
   }
-  g.a = in ? in : w.pl; g.a_lo_off = (int64_t)B * T * cw.w.cpad;
+  g = plane_args(cw, w, B, T, dil, res, out, out_scale, accumulate, out_act, prec, in);
   if (act) {
     g.act_plane = act_out;
     g.act_plane_lo_off = (int64_t)B * T * round_up(cw.w.rows, 32);
@@ -1395,11 +1409,6 @@ static int plane_conv(hipStream_t s, const ConvW& cw, const VocWs& w, int B, int
     g.act_up_filter = act->fup;
     g.act_down_filter = act->fdn;
   }
-  g.B = B; g.T = T; g.C = cw.w.cin; g.Cp = cw.w.cpad;
-  g.ksize = cw.w.taps; g.dil = dil; g.pad = (cw.w.taps - 1) * dil / 2;
-  g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
-  g.bias = cw.b; g.res = res; g.out = out; g.out_act = out_act; g.accumulate = accumulate;
-  g.out_scale = out_scale; g.prec = prec;
   g.out_plane = out_plane;
   return opconv(g, s);
 }
@@ -1503,6 +1512,11 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
       ALCM_HIP(hipEventRecord(ax->ev[0], s));
       for (auto a : ax->s) ALCM_HIP(hipStreamWaitEvent(a, ax->ev[0], 0));
     }
+    // the wide stages' mean over the three chains in one sum-form launch of their last conv2 + residual
+    // (alcm_opconv_sum): x written once, not read and rewritten per chain (ALCM_WCONV_SUM=0: three accumulating
+    // launches, the chains' last convs in order)
+    const bool sum3 = !fuse && S.rb.size() == 3 && (conc || act3) && knobs().wconv_sum;
+    alcm_opconv_args lastc[3];
     for (size_t j = 0; j < S.rb.size(); ++j) {
       const AmpW& A = S.rb[j];
       const VocChain& cb = w.ch[(conc || act3) ? j : 0];
@@ -1512,7 +1526,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
       for (size_t l = 0; l < A.dil.size(); ++l) {
         const bool last = l + 1 == A.dil.size();
         // the mean over resblocks accumulates into x: the chains' last convs run in order (j-1 before j)
-        if (last && conc && j > 0) ALCM_HIP(hipStreamWaitEvent(sj, ax->ev[j], 0));
+        if (last && conc && j > 0 && !sum3) ALCM_HIP(hipStreamWaitEvent(sj, ax->ev[j], 0));
         if (fuse) {
           if (l == 0 && !act3) ALCM_TRY(act_planes(sj, A.act[0], cur, w, B, To, S.cout, pamp, cb.pl));
           ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, nullptr, 1.f, 0, 0, pamp, cb.pl,
@@ -1540,14 +1554,23 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
             ALCM_TRY(plane_conv(sj, A.c1[l], w, B, To, A.dil[l], nullptr, cb.t, 1.f, 0, 0, pamp, cb.pl));
             ALCM_TRY(act_planes(sj, A.act[2 * l + 1], cb.t, w, B, To, S.cout, pamp, cb.pl));
           }
-          ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, last ? x : cb.rb, last ? inv : 1.f, last && j > 0, 0,
-                              pamp, cb.pl));
+          if (last && sum3)
+            lastc[j] = plane_args(A.c2[l], w, B, To, 1, cur, j == 0 ? x : nullptr, inv, 0, 0, pamp, cb.pl);
+          else
+            ALCM_TRY(plane_conv(sj, A.c2[l], w, B, To, 1, cur, last ? x : cb.rb, last ? inv : 1.f, last && j > 0, 0,
+                                pamp, cb.pl));
           cur = cb.rb;
         }
         if (last && conc) ALCM_HIP(hipEventRecord(ax->ev[j + 1], sj));
       }
     }
-    if (conc) ALCM_HIP(hipStreamWaitEvent(s, ax->ev[S.rb.size()], 0));  // the stage output is complete
+    if (sum3) {
+      if (conc)
+        for (size_t j = 1; j < S.rb.size(); ++j) ALCM_HIP(hipStreamWaitEvent(s, ax->ev[j + 1], 0));
+      ALCM_TRY(opconv_sum(lastc, 3, s));
+    } else if (conc) {
+      ALCM_HIP(hipStreamWaitEvent(s, ax->ev[S.rb.size()], 0));  // the stage output is complete
+    }
     T = To;
   }
   // activation_post -> conv_post k7 -> tanh (models.py:201-203)

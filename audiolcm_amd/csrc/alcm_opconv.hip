@@ -720,7 +720,35 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
   return 0;
 }
 
+// out = (sum over i < n of conv_i + bias_i + res_i) * args[0].out_scale (+ out if args[0].accumulate): the fused
+// sum-form launch where it applies (three wide terms), else the terms in order, each accumulating into out
+int opconv_sum(const alcm_opconv_args* a, int n, hipStream_t s) {
+  if (!a || n < 1 || n > 3) return set_error(ALCM_E_INVALID, "opconv_sum: 1 <= n <= 3 terms");
+  if (!a[0].out) return set_error(ALCM_E_INVALID, "opconv_sum: args[0].out is required");
+  for (int i = 0; i < n; ++i)
+    if (a[i].B != a[0].B || a[i].T != a[0].T || a[i].N != a[0].N || a[i].act_plane || a[i].out_plane ||
+        a[i].geglu_plane || a[i].out_stride > 0 || a[i].out_act || (a[i].out && a[i].out != a[0].out))
+      return set_error(ALCM_E_INVALID, "opconv_sum: terms need equal B, T, N, same-length fp32 outputs into "
+                                       "args[0].out, no activation / plane / GEGLU / strided output");
+  if (wconv3_sum_try(a, n, s)) {
+    ALCM_HIP(hipGetLastError());
+    return 0;
+  }
+  for (int i = 0; i < n; ++i) {
+    alcm_opconv_args g = a[i];
+    g.out = a[0].out;
+    g.out_scale = a[0].out_scale;
+    g.accumulate = i > 0 ? 1 : a[0].accumulate;
+    ALCM_TRY(opconv(g, s));
+  }
+  return 0;
+}
+
 }  // namespace alcm
+
+extern "C" int alcm_opconv_sum(const alcm_opconv_args* args, int n, alcm_stream_t stream) {
+  return alcm::opconv_sum(args, n, (hipStream_t)stream);
+}
 
 extern "C" int alcm_activation1d_op(const float* x, void* y, int B, int T, int C, int Cp, const float* alpha_exp,
                                     const float* inv_beta, const float* up_filter, const float* down_filter, int prec,

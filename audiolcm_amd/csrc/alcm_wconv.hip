@@ -42,6 +42,15 @@ struct WConvDev {
   int ksplit;           // wconv3: > 1 = the 64-channel chunks split into ksplit contiguous parts, one work item per
                         // (tile, part); each item writes its fp32 partial sums to part + kpart * B T N (no epilogue)
   float* part;
+  // wconv3 sum form (nseg > 1): out = (sum over s < nseg of conv_s(sa[s], sw[s]) + sbias[s] + sres[s]) * out_scale
+  // (+ out): the AMPBlock chains' last conv2 + residual of a stage in one pass (models.py:190-199), every term with
+  // the same T, Cp, N and dilation 1, its own plane, weights, taps, bias and residual
+  int nseg;
+  const u16* sa[3];
+  const u16* sw[3];
+  int sk[3], spad[3], skpad[3];
+  const float* sbias[3];
+  const float* sres[3];
 };
 
 
@@ -366,7 +375,11 @@ __device__ __forceinline__ void w3_wait_barrier() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
   __builtin_amdgcn_s_barrier();
 }
-template <int PREC>
+template <typename V>
+__device__ __forceinline__ V w3_sel(const V (&v)[3], int i) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
+}
+template <int PREC, int SEG>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
@@ -385,10 +398,11 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   const int first = tbeg + slot;
   const int my_n = first < tend ? (tend - first + nslot - 1) / nslot : 0;
   if (my_n == 0) return;
-  const int K = P.ksize, Cp = P.Cp, nC = Cp / 64 / KS;  // 64-channel chunks per item
-  const int WR = W3_BM + (K - 1) * P.dil;
-  const int total = my_n * nC * K;   // steps
-  const int nchunks = my_n * nC;     // windows
+  const int Cp = P.Cp, nC = Cp / 64 / KS;  // 64-channel chunks per item and term
+  // SEG > 1: a tile's chunks are the terms' chunks in order (term s: chunks s nC .. s nC + nC - 1, P.sk[s] taps each)
+  const int NCH = SEG * nC;
+  const int total = my_n * nC * (SEG == 1 ? P.ksize : P.sk[0] + P.sk[1] + (SEG > 2 ? P.sk[2] : 0));  // steps
+  const int nchunks = my_n * NCH;  // windows
   const int tiles_m = ntiles / P.tiles_n;
   auto tile_of = [&](int ti, int& b, int& t0, int& col0, int& kp) {
     int tile = first + ti * nslot;
@@ -411,12 +425,22 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   const u16* wsrc_base = P.a;  // batch b, channel chunk c
   int wrow0 = 0;               // first window row's time index (t0 - pad)
   int wbuf = 0;
+  int WR = W3_BM + (P.ksize - 1) * P.dil;  // window rows of the chunk being staged
   auto win_setup = [&](int q) {
-    const int ti = q / nC, c = q - ti * nC;
+    const int ti = q / NCH;
+    int c = q - ti * NCH;
     int b, t0, col0, kp;
     tile_of(ti, b, t0, col0, kp);
-    wsrc_base = P.a + (int64_t)b * P.T * Cp + (kp * nC + c) * 64;
-    wrow0 = t0 - P.pad;
+    if constexpr (SEG == 1) {
+      wsrc_base = P.a + (int64_t)b * P.T * Cp + (kp * nC + c) * 64;
+      wrow0 = t0 - P.pad;
+    } else {
+      const int sg = c / nC;
+      c -= sg * nC;
+      wsrc_base = w3_sel(P.sa, sg) + (int64_t)b * P.T * Cp + c * 64;
+      wrow0 = t0 - w3_sel(P.spad, sg);
+      WR = W3_BM + w3_sel(P.sk, sg) - 1;
+    }
     wbuf = q & 1;
   };
   auto win_piece = [&](int j) {
@@ -437,42 +461,63 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   // behind it (a burst every 11 steps cost 12 % in scripts/probes/mfma_lds_probe.hip); issued no later than tap
   // K - 3, every piece is covered by the counted wait at the chunk's last mid-step (a burst at the chunk's first
   // step measured equal within 2 %)
-  const int wspread = K - 2;
+  int K = SEG == 1 ? P.ksize : P.sk[0];  // taps of the chunk being computed
+  int wspread = K - 2;
 
   // weight DMA: per-lane 32-bit byte offsets (row n * kpad + 16-B piece) from a workgroup-uniform base, so each
   // instruction is a saddr + voffset access with no per-step 64-bit address arithmetic; instruction j covers rows
   // 8 (wave + 8 j) .. + 7
   uint32_t boff[W3_BPW];
+  auto set_boff = [&](int kpad) {
 #pragma unroll
-  for (int j = 0; j < W3_BPW; ++j) {
-    const int n = 8 * (wave + 8 * j) + (lane >> 3);
-    boff[j] = (uint32_t)(n * P.kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
-  }
+    for (int j = 0; j < W3_BPW; ++j) {
+      const int n = 8 * (wave + 8 * j) + (lane >> 3);
+      boff[j] = (uint32_t)(n * kpad + ((lane & 7) ^ (n & 7)) * 8) * 2u;
+    }
+  };
+  set_boff(SEG == 1 ? P.kpad : P.skpad[0]);
   // issue cursor: weight step ig = (tile iti, chunk ic, tap itap) at element offset iwoff of the weight plane; past
   // the last step it stays on the last tile (the ring slot it refills is never read again)
   int ig = 0, ic = 0, itap = 0, iti = 0;
   int64_t iwoff;
+  int icol0;                                           // the issue tile's first column
+  int iK = SEG == 1 ? P.ksize : P.sk[0];               // the issue step's term: taps, weight plane
+  const u16* iw = SEG == 1 ? P.w : P.sw[0];
   {
-    int b_, t0_, col0_, kp_;
-    tile_of(0, b_, t0_, col0_, kp_);
-    iwoff = (int64_t)col0_ * P.kpad + kp_ * nC * 64;
+    int b_, t0_, kp_;
+    tile_of(0, b_, t0_, icol0, kp_);
+    iwoff = (int64_t)icol0 * (SEG == 1 ? P.kpad : P.skpad[0]) + kp_ * nC * 64;
   }
   auto issue_wt = [&](int sl) {
-    const char* base = reinterpret_cast<const char*>(P.w + iwoff);
+    const char* base = reinterpret_cast<const char*>(iw + iwoff);
 #pragma unroll
     for (int j = 0; j < W3_BPW; ++j) glds16(base + boff[j], smem + 2 * W3_WBUF + sl * W3_BBUF + (wave + 8 * j) * 1024);
   };
   auto advance_wt = [&]() {
     if (++ig >= total) return;
     iwoff += Cp;
-    if (++itap == K) {
+    if (++itap == iK) {
       itap = 0;
-      iwoff += 64 - (int64_t)K * Cp;
-      if (++ic == nC) {
+      iwoff += 64 - (int64_t)iK * Cp;
+      if (++ic == NCH) {
         ic = 0;
-        int b_, t0_, col0_, kp_;
-        tile_of(++iti, b_, t0_, col0_, kp_);
-        iwoff = (int64_t)col0_ * P.kpad + kp_ * nC * 64;
+        int b_, t0_, kp_;
+        tile_of(++iti, b_, t0_, icol0, kp_);
+        if constexpr (SEG == 1) {
+          iwoff = (int64_t)icol0 * P.kpad + kp_ * nC * 64;
+        } else {
+          iK = P.sk[0];
+          iw = P.sw[0];
+          set_boff(P.skpad[0]);
+          iwoff = (int64_t)icol0 * P.skpad[0];
+        }
+      } else if (SEG > 1 && ic % nC == 0) {  // the next term's first chunk
+        const int sg = ic / nC;
+        iK = w3_sel(P.sk, sg);
+        iw = w3_sel(P.sw, sg);
+        const int kp = w3_sel(P.skpad, sg);
+        set_boff(kp);
+        iwoff = (int64_t)icol0 * kp;
       }
     }
   };
@@ -510,6 +555,48 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     const bool accum = !split && P.accumulate;
     const float oscale = split ? 1.f : P.out_scale;
     float bv[TN];
+    if constexpr (SEG > 1) {
+      // sum form: (acc + (b_0 + b_1 + b_2) + ((r_0 + r_1) + r_2)) * scale (+ out)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + wn * 96 + j * 16 + (lane & 15);
+        float v = 0.f;
+#pragma unroll
+        for (int sg = 0; sg < SEG; ++sg) v += P.sbias[sg] ? P.sbias[sg][col] : 0.f;
+        bv[j] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int rh = 0; rh < 4; rh += 2) {  // row pairs: 3 residual reads per output
+          float rv[2][TN], pv[2][TN];
+          int orow[2];
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + rh + r;
+            orow[r] = t < P.T ? b * P.T + t : -1;
+            const int64_t ro = (int64_t)max(orow[r], 0) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              float v = P.sres[0] ? P.sres[0][ro + j * 16] : 0.f;
+#pragma unroll
+              for (int sg = 1; sg < SEG; ++sg) v += P.sres[sg] ? P.sres[sg][ro + j * 16] : 0.f;
+              rv[r][j] = v;
+              pv[r][j] = accum ? outp[ro + j * 16] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            if (orow[r] < 0) continue;
+            const int64_t ro = (int64_t)orow[r] * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              outp[ro + j * 16] = (acc[i][j][rh + r] + bv[j] + rv[r][j]) * oscale + pv[r][j];
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) bv[j] = (P.bias && !split) ? P.bias[col0 + wn * 96 + j * 16 + (lane & 15)] : 0.f;
     if (P.oplane) {
@@ -656,7 +743,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
     }
     tap = 0;
     ++q;
-    if (++c == nC) {
+    if (++c == NCH) {
       epilogue(ti);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -664,6 +751,10 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       c = 0;
       ++ti;
+    }
+    if constexpr (SEG > 1) {  // the next chunk's term
+      K = w3_sel(P.sk, c / nC);
+      wspread = K - 2;
     }
   }
 }
@@ -764,8 +855,8 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16>), dim3(grid), dim3(512), 0, s, P);
-  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16>), dim3(grid), dim3(512), 0, s, P);
+  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 1>), dim3(grid), dim3(512), 0, s, P);
   if (ks > 1) ksplit_reduce(a, ks, s);
   if (tok) {
     char name[96];
@@ -774,6 +865,77 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
+    prof_stop(tok, s, name, flops, bytes);
+  }
+  return 1;
+}
+
+// Sum form (alcm_opconv_sum): three same-length terms with their own planes, weights, taps, biases and residuals
+// into one output, one pass of the persistent kernel and one epilogue (out = (sum of the terms' conv + bias +
+// residual) * scale (+ out)).  Eligible: the terms' shared B, T, Cp, N and precision (F16 / BF16), dilation 1,
+// 3 <= k <= 65, Cp % 64 == 0, N % 192 == 0, full 256-row tiles filling the chip (as wconv3 by shape).  Returns 1
+// when it launched.
+int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
+  if (n != 3 || knobs().wconv_sum == 0 || knobs().wconv <= 0 || knobs().wconv3 == 0) return 0;
+  const alcm_opconv_args& a0 = a[0];
+  if ((a0.prec != PREC_F16 && a0.prec != PREC_BF16) || !a0.out || a0.Cp % 64 || a0.N % W3_BN) return 0;
+  for (int i = 0; i < n; ++i) {
+    const alcm_opconv_args& t = a[i];
+    if (t.B != a0.B || t.T != a0.T || t.Cp != a0.Cp || t.N != a0.N || t.prec != a0.prec || t.dil != 1 ||
+        t.ksize < 3 || t.ksize - 1 > 64 || 2 * t.pad != t.ksize - 1 || t.out_act || t.out_stride > 0 ||
+        t.geglu_plane || t.out_plane || t.act_plane || (int64_t)W3_BN * t.kpad * 2 >= (1ll << 31))
+      return 0;
+  }
+  if (!g_ncu) {
+    int dev = 0, nc = 0;
+    g_ncu = (hipGetDevice(&dev) == hipSuccess &&
+             hipDeviceGetAttribute(&nc, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && nc >= 8)
+                ? nc
+                : 256;
+  }
+  const int mt256 = (a0.T + W3_BM - 1) / W3_BM;
+  const int64_t nt = (int64_t)a0.B * mt256 * (a0.N / W3_BN);
+  const bool full = a0.T * 100 >= mt256 * W3_BM * 85;
+  if (!(knobs().wconv3 > 0 || (full && nt >= g_ncu))) return 0;
+  if (nt >= (1ll << 30) || (int64_t)a0.B * a0.T * a0.Cp >= (1ll << 40) || (int64_t)a0.B * a0.T * a0.N >= (1ll << 40))
+    return 0;
+  WConvDev P{};
+  P.a = (const u16*)a0.a;
+  P.T = a0.T; P.Cp = a0.Cp; P.ksize = a0.ksize; P.dil = 1; P.pad = a0.pad;
+  P.N = a0.N;
+  P.out = a0.out; P.out_scale = a0.out_scale; P.accumulate = a0.accumulate;
+  P.tiles_per_batch = mt256;
+  P.tiles_n = a0.N / W3_BN;
+  P.nwg = (int)nt;
+  P.n_major = 1;
+  P.nseg = n;
+  double flops = 0, bytes = (double)a0.B * a0.T * a0.N * 4.0 * (a0.accumulate ? 2 : 1);
+  for (int i = 0; i < n; ++i) {
+    const bool f16 = a[i].prec == PREC_F16;
+    P.sa[i] = (const u16*)a[i].a;
+    P.sw[i] = (const u16*)a[i].w + (f16 ? 2 * a[i].w_lo_off : 0);
+    P.sk[i] = a[i].ksize;
+    P.spad[i] = a[i].pad;
+    P.skpad[i] = a[i].kpad;
+    P.sbias[i] = a[i].bias;
+    P.sres[i] = a[i].res;
+    flops += 2.0 * a0.B * a0.T * a0.N * (double)a[i].ksize * a[i].C;
+    bytes += (double)a0.B * a0.T * a0.Cp * 2.0 + (double)a0.N * a[i].kpad * 2.0 +
+             (a[i].res ? (double)a0.B * a0.T * a0.N * 4.0 : 0.0);
+  }
+  P.w = P.sw[0]; P.kpad = P.skpad[0];
+  const int R = (int)((nt + 7) / 8);
+  int grid = 8 * std::min(g_ncu / 8, R);
+  if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
+  void* tok = prof_start(s);
+  if (a0.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 3>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 3>), dim3(grid), dim3(512), 0, s, P);
+  if (tok) {
+    char name[96];
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, sum3>", a0.prec);
+    if (knobs().prof_shapes)
+      std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d+%d+%d", a0.T, a0.Cp,
+                    a0.N, a[0].ksize, a[1].ksize, a[2].ksize);
     prof_stop(tok, s, name, flops, bytes);
   }
   return 1;

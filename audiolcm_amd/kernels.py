@@ -358,6 +358,42 @@ def activation1d_op_f16in(x16: torch.Tensor, alpha: torch.Tensor, beta: torch.Te
     return y
 
 
+def opconv_sum(terms, prec: int, out_scale: float = 1.0, accumulate_into: Optional[torch.Tensor] = None):
+    """alcm_opconv_sum: out (B, T, N) = (sum over terms of conv_k(planes) + bias + residual) * out_scale (+ out) — the
+    mean over a BigVGAN stage's resblocks at their last conv2 + residual (vocoder/bigvgan/models.py:190-199).
+    terms: up to three (planes (1, B, T, Cp), w (N, C, k), bias or None, residual (B, T, N) or None, packed or None),
+    same-length dilation-1 convs sharing B, T and N."""
+    n = len(terms)
+    assert 1 <= n <= 3
+    args = (_hip.OpConvArgs * n)()
+    keep = []
+    out = None
+    for i, (planes, w, bias, res, packed) in enumerate(terms):
+        npl, B, T, Cp = planes.shape
+        assert planes.dtype == torch.int16 and planes.is_contiguous()
+        N, cin, k = w.shape
+        if packed is None:
+            wp = torch.nn.functional.pad(w, (0, 0, 0, Cp - cin)).contiguous() if Cp != cin else w
+            packed = pack_conv_weight(wp)
+        keep.append(packed)
+        if out is None:
+            out = accumulate_into if accumulate_into is not None else torch.empty((B, T, N), device=planes.device)
+        a = args[i]
+        a.a, a.a_lo_off, a.B, a.T, a.C, a.Cp = ptr(planes), B * T * Cp, B, T, cin, Cp
+        a.ksize, a.dil, a.pad = k, 1, (k - 1) // 2
+        a.w, a.w_lo_off, a.kpad, a.N = ptr(packed.data), packed.lo_off, packed.kpad, N
+        a.bias = ptr(bias)
+        if res is not None:
+            res = res.contiguous()
+            keep.append(res)
+        a.res = ptr(res)
+        a.prec = int(prec)
+        if i == 0:
+            a.out, a.out_scale, a.accumulate = ptr(out), out_scale, int(accumulate_into is not None)
+    check(lib().alcm_opconv_sum(args, n, stream_handle()), "opconv_sum")
+    return out
+
+
 def opconv(planes: torch.Tensor, C_real: int, w: torch.Tensor, bias: Optional[torch.Tensor], dilation: int,
            prec: int, residual: Optional[torch.Tensor] = None, out_act: int = 0, out_scale: float = 1.0,
            accumulate_into: Optional[torch.Tensor] = None, packed: Optional["PackedWeight"] = None,

@@ -224,6 +224,16 @@ typedef struct alcm_opconv_args {
   int64_t ksplit_ws_floats;
 } alcm_opconv_args;
 int alcm_opconv(const alcm_opconv_args* args, alcm_stream_t stream);
+/* alcm_opconv_sum: out = (sum over i < n of conv_i(args[i].a) + args[i].bias + args[i].res) * args[0].out_scale
+ *   (+ out when args[0].accumulate), 1 <= n <= 3 — the mean over a BigVGAN stage's resblocks (vocoder/bigvgan/
+ *   models.py:190-199: xs += resblock_j(x); x = xs / num_kernels) taken at the chains' last conv2 + residual
+ *   (models.py:76-80), so the stage output is written once instead of read and rewritten per chain.  Each term is
+ *   an alcm_opconv same-length conv with its own planes, weights, ksize / pad, bias and residual; the terms share B,
+ *   T and N, and only args[0]'s out / out_scale / accumulate are read (another term's out must be NULL or the same).
+ *   Three F16 / BF16 terms of dilation 1 with Cp % 64 == 0 and N % 192 == 0 run as one launch summing all taps in one
+ *   fp32 accumulator; otherwise the terms run in order, each accumulating into out (the same value up to fp32
+ *   rounding order).  No activation / plane / GEGLU / strided outputs. */
+int alcm_opconv_sum(const alcm_opconv_args* args, int n, alcm_stream_t stream);
 /* alcm_opconv_dense: the narrow AMPBlock conv of BigVGAN stages 3-5 (vocoder/bigvgan/models.py:72-81, C = N in
  * {24, 48} at F16 / F16W2, 96 at F16; ksize <= 11, (ksize-1)*dil <= 64) with the weights resident in LDS: same
  * arguments as alcm_opconv except that w is packed by alcm_pack_conv_weight with cpad = C (dense K = tap*C + c,

@@ -925,3 +925,48 @@ def test_wconv2_ksplit_text_linears(K, C, N):
     e_s, e_r = rel_l2(ys.numpy(), y1.numpy()), rel_l2(ys[0].numpy(), ref.numpy())
     print(f"wconv2 ksplit C{C} N{N}: split vs unsplit {e_s:.2e}, vs F.linear {e_r:.2e}")
     assert e_s < 1e-6 and e_r < 1e-5
+
+
+@pytest.mark.parametrize("C,T,grid,acc", [(384, 1100, 0, False), (192, 1500, 16, True), (768, 600, 8, False)])
+def test_opconv_sum_three_chains(K, C, T, grid, acc, monkeypatch):
+    """alcm_opconv_sum: a BigVGAN stage's mean over its three resblocks taken at the chains' last conv2 + residual
+    (vocoder/bigvgan/models.py:190-199 with AMPBlock1's conv2 + x, models.py:76-80): k = 3 / 7 / 11 terms with their
+    own planes, weights, biases and residuals summed in one persistent launch (ALCM_WCONV3_GRID caps the workgroups
+    so each walks several tiles across the terms' window / weight switches) vs F.conv1d on the fp16 operands and vs
+    the three accumulating launches (ALCM_WCONV_SUM=0: fp32 rounding order only)."""
+    from audiolcm_amd import _hip
+    B, inv = 2, 1.0 / 3
+    ks = (3, 7, 11)
+    xs = [_r((B, T, C), 210 + i, 0.5) for i in range(3)]
+    ws = [_r((C, C, k), 213 + i, 1.0 / np.sqrt(C * k)) for i, k in enumerate(ks)]
+    bs = [_r((C,), 216 + i, 0.05) for i in range(3)]
+    rs = [_r((B, T, C), 219 + i) for i in range(3)]
+    o0 = _r((B, T, C), 222)
+    pls = [K.operand_planes(dev(x), 2) for x in xs]
+    pws = [K.pack_conv_weight(dev(w)) for w in ws]
+    terms = [(pls[i], dev(ws[i]), dev(bs[i]), dev(rs[i]), pws[i]) for i in range(3)]
+    outs, names = [], []
+    for sm in ("1", "0"):
+        env = {"ALCM_WCONV_SUM": sm, "ALCM_WCONV3": "1", "ALCM_WCONV3_GRID": str(grid), "ALCM_PROF_SHAPES": "1"}
+        for kk, v in env.items():
+            monkeypatch.setenv(kk, v)
+        _hip.reload_knobs()
+        try:
+            _hip.profile_begin()
+            y = K.opconv_sum(terms, 2, out_scale=inv, accumulate_into=dev(o0.clone()) if acc else None)
+            torch.cuda.synchronize()
+            names.append([p["name"] for p in _hip.profile_end()])
+            outs.append(y.cpu())
+        finally:
+            for kk in env:
+                monkeypatch.delenv(kk)
+            _hip.reload_knobs()
+    assert any("sum3" in n for n in names[0]), names[0]
+    assert not any("sum3" in n for n in names[1]), names[1]
+    ref = sum(F.conv1d(xs[i].half().float().permute(0, 2, 1), ws[i].half().float(), bs[i],
+                       padding=(ks[i] - 1) // 2).permute(0, 2, 1) + rs[i] for i in range(3)) * inv
+    if acc:
+        ref = ref + o0
+    e_ref, e_seq = rel_l2(outs[0].numpy(), ref.numpy()), rel_l2(outs[0].numpy(), outs[1].numpy())
+    print(f"opconv_sum C{C} T{T}: vs F.conv1d {e_ref:.2e}, vs three launches {e_seq:.2e}")
+    assert e_ref < 1e-5 and e_seq < 1e-6
