@@ -79,6 +79,7 @@ int flash_attention(const float* qkv, float* O, int B, int L, int H, int nh, int
                     const void* qkv_plane = nullptr);
 // whether opconv can fuse Activation1d into its epilogue for N output channels at this precision
 bool opconv_act_supported(int prec, int N, int Cp_in);
+bool wconv3_sum_ok(const alcm_opconv_args* a, int n);
 int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s);
 int opconv_sum(const alcm_opconv_args* a, int n, hipStream_t s);
 int wconv_try(const alcm_opconv_args& a, const unsigned short* wplane, double flops, double bytes,
@@ -130,7 +131,8 @@ struct Knobs {
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
   int act_x3_mfma = 1;           // ALCM_ACT_X3_MFMA: the wide stages' three first Activation1d in one MFMA-FIR pass (0 = three)
   int wconv_sum = 1;             // ALCM_WCONV_SUM: the wide stages' three chains' last conv2 + residual in one sum-form
-                                 // launch (0 = three accumulating launches)
+                                 // launch writing the next stage's upsampler planes (2 = fp32 output + to_planes,
+                                 // 0 = three accumulating launches)
   int ksplit = 1;                // ALCM_KSPLIT: wconv3 K parts on under-filled grids where a workspace is given (0 = never)
   int xp[4] = {0, 0, 0, 0};      // ALCM_XP0..3: scratch switches for an experiment in flight (no default path reads them)
 };

@@ -1435,22 +1435,28 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   float* u = w.y;
   float* rb = w.rb;
   float* y = w.t;
+  // stage si's upsampler runs on operand planes of its input (mixed policy: stages 0-3, +1.9e-4 waveform rel-L2
+  // emulated, scripts/precision_emulate.py 96 tail): a plane conv of x with a strided epilogue (the wide-layer kernel
+  // for N % 192 == 0, opconv_kernel for N <= 96) — the same eligibility opconv's strided paths check (the wide-layer
+  // kernel needs Cp % 64 == 0 and a tap window of at most 64 rows; otherwise the fp32-operand phase conv below)
+  auto ups_planes_of = [&](size_t si) {
+    const StageW& S = G.st[si];
+    const int pamp = voc_prec(m, (int)si);
+    const bool wide_ok = S.cout % 192 == 0 && S.cin % 64 == 0 && S.phase[0].w.taps - 1 <= 64;
+    return (pamp == PREC_F16 || pamp == PREC_BF16) && S.cin % 32 == 0 &&
+           (wide_ok || (S.cout <= 96 && S.cout % 4 == 0)) && S.phase[0].w.cpad == S.cin;
+  };
+  const u16* xpl = nullptr;  // the stage input's planes when the previous stage's sum-form conv wrote them
   for (size_t si = 0; si < G.st.size(); ++si) {
     const StageW& S = G.st[si];
     const int To = T * S.rate;
     const int pamp = voc_prec(m, (int)si);
-    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188).  Stages whose AMP convs run
-    // on single fp16 / bf16 planes (mixed policy: stages 0-3, +1.9e-4 waveform rel-L2 emulated,
-    // scripts/precision_emulate.py 96 tail) take a plane conv of x with a strided epilogue (the wide-layer
-    // kernel for N % 192 == 0, opconv_kernel for N <= 96); the others the fp32-operand conv at the base
-    // precision
-    // (the same eligibility opconv's strided paths check: the wide-layer kernel needs Cp % 64 == 0 and a tap
-    // window of at most 64 rows; otherwise the fp32-operand phase conv below, never a hard error)
-    const bool wide_ok = S.cout % 192 == 0 && S.cin % 64 == 0 && S.phase[0].w.taps - 1 <= 64;
-    const bool ups_planes = (pamp == PREC_F16 || pamp == PREC_BF16) && S.cin % 32 == 0 &&
-                            (wide_ok || (S.cout <= 96 && S.cout % 4 == 0)) &&
-                            S.phase[0].w.cpad == S.cin;
-    if (ups_planes) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
+    // ConvTranspose1d as S.rate phase convolutions (models.py:160-165, 187-188): on operand planes of x where
+    // ups_planes_of(si), the fp32-operand conv at the base precision otherwise
+    const bool ups_planes = ups_planes_of(si);
+    const u16* upl = xpl ? xpl : w.pl;
+    if (ups_planes && !xpl) ALCM_TRY(to_planes(x, w.pl, (int64_t)B * T, S.cin, S.cin, pamp, s));
+    xpl = nullptr;
     // the split-precision stride-2 stages with the kernel's widths (stages 4-5): both phases in one pass over x
     const bool ups_two = !ups_planes && split == PREC_SPLIT && S.rate == 2 &&
                          ups2_supported(S.cin, S.cout, S.phase[0].w.cpad, S.rate, S.phase[0].w.taps) &&
@@ -1463,7 +1469,7 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
         const ConvW& cw = S.phase[r];
         alcm_opconv_args g;
         std::memset(&g, 0, sizeof(g));
-        g.a = w.pl; g.a_lo_off = (int64_t)B * T * S.cin;
+        g.a = upl; g.a_lo_off = (int64_t)B * T * S.cin;
         g.B = B; g.T = T; g.C = S.cin; g.Cp = S.cin;
         g.ksize = cw.w.taps; g.dil = 1; g.pad = S.pad[r];
         g.w = cw.w.p; g.w_lo_off = cw.w.lo; g.kpad = cw.w.kpad; g.N = cw.w.rows;
@@ -1567,6 +1573,19 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
     if (sum3) {
       if (conc)
         for (size_t j = 1; j < S.rb.size(); ++j) ALCM_HIP(hipStreamWaitEvent(s, ax->ev[j + 1], 0));
+      // the next stage's upsampler reads only the operand planes of this output: the sum-form epilogue writes them
+      // (the rounding to_planes applies to the fp32 value, bit for bit) into chain 0's spare plane buffer, free
+      // until the next stage's chains start
+      if (knobs().wconv_sum == 1 && si + 1 < G.st.size() && ups_planes_of(si + 1) && voc_prec(m, (int)si + 1) == pamp &&
+          G.st[si + 1].cin == S.cout) {
+        alcm_opconv_args pc[3] = {lastc[0], lastc[1], lastc[2]};
+        pc[0].out = nullptr;
+        pc[0].out_plane = w.ch[0].pl2;
+        if (wconv3_sum_ok(pc, 3)) {
+          lastc[0] = pc[0];
+          xpl = w.ch[0].pl2;
+        }
+      }
       ALCM_TRY(opconv_sum(lastc, 3, s));
     } else if (conc) {
       ALCM_HIP(hipStreamWaitEvent(s, ax->ev[S.rb.size()], 0));  // the stage output is complete

@@ -724,9 +724,12 @@ int opconv(const alcm_opconv_args& a, hipStream_t s) {
 // sum-form launch where it applies (three wide terms), else the terms in order, each accumulating into out
 int opconv_sum(const alcm_opconv_args* a, int n, hipStream_t s) {
   if (!a || n < 1 || n > 3) return set_error(ALCM_E_INVALID, "opconv_sum: 1 <= n <= 3 terms");
-  if (!a[0].out) return set_error(ALCM_E_INVALID, "opconv_sum: args[0].out is required");
+  if (!a[0].out && !a[0].out_plane) return set_error(ALCM_E_INVALID, "opconv_sum: args[0].out is required");
+  if (a[0].out_plane && !wconv3_sum_ok(a, n))
+    return set_error(ALCM_E_INVALID, "opconv_sum: a plane output needs the one-launch form (three F16 / BF16 terms, "
+                                     "dilation 1, Cp % 64 == 0, N % 192 == 0, full 256-row tiles) and no accumulate");
   for (int i = 0; i < n; ++i)
-    if (a[i].B != a[0].B || a[i].T != a[0].T || a[i].N != a[0].N || a[i].act_plane || a[i].out_plane ||
+    if (a[i].B != a[0].B || a[i].T != a[0].T || a[i].N != a[0].N || a[i].act_plane || (i > 0 && a[i].out_plane) ||
         a[i].geglu_plane || a[i].out_stride > 0 || a[i].out_act || (a[i].out && a[i].out != a[0].out))
       return set_error(ALCM_E_INVALID, "opconv_sum: terms need equal B, T, N, same-length fp32 outputs into "
                                        "args[0].out, no activation / plane / GEGLU / strided output");

@@ -565,6 +565,44 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
         for (int sg = 0; sg < SEG; ++sg) v += P.sbias[sg] ? P.sbias[sg][col] : 0.f;
         bv[j] = v;
       }
+      if (P.oplane) {
+        // the stage output as the next stage's operand plane (its only consumer, the upsampler, reads that format):
+        // fp16 / bf16 of the fp32 value the fp32 route stores ((acc + b + r) * scale + 0), column pairs by DPP
+        const bool odd = lane & 1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const int r = 2 * rp + (odd ? 1 : 0);
+            const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            const int64_t rb = ((int64_t)b * P.T + min(t, P.T - 1)) * P.N + col0 + wn * 96;
+            float rv[2][TN];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // rows 2 rp (h = 0) and 2 rp + 1 of this lane's column
+              const int64_t ro = ((int64_t)b * P.T + min(t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + 2 * rp + h,
+                                                         P.T - 1)) * P.N + col0 + wn * 96 + (lane & 15);
+#pragma unroll
+              for (int j = 0; j < TN; ++j) {
+                float v = P.sres[0] ? P.sres[0][ro + j * 16] : 0.f;
+#pragma unroll
+                for (int sg = 1; sg < SEG; ++sg) v += P.sres[sg] ? P.sres[sg][ro + j * 16] : 0.f;
+                rv[h][j] = v;
+              }
+            }
+            u16* const rowp = P.oplane + rb + (lane & 14);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const float v0 = (acc[i][j][2 * rp] + bv[j] + rv[0][j]) * oscale + 0.f;
+              const float v1 = (acc[i][j][2 * rp + 1] + bv[j] + rv[1][j]) * oscale + 0.f;
+              const float send = odd ? v0 : v1;
+              const float recv = __builtin_bit_cast(
+                  float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, true));
+              const float lo = odd ? recv : v0, hi = odd ? v1 : recv;
+              if (t < P.T) op_store2<PREC>(rowp + j * 16, 0, f32x2{lo, hi});
+            }
+          }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -875,16 +913,18 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
 // residual) * scale (+ out)).  Eligible: the terms' shared B, T, Cp, N and precision (F16 / BF16), dilation 1,
 // 3 <= k <= 65, Cp % 64 == 0, N % 192 == 0, full 256-row tiles filling the chip (as wconv3 by shape).  Returns 1
 // when it launched.
-int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
-  if (n != 3 || knobs().wconv_sum == 0 || knobs().wconv <= 0 || knobs().wconv3 == 0) return 0;
+bool wconv3_sum_ok(const alcm_opconv_args* a, int n) {
+  if (n != 3 || knobs().wconv_sum == 0 || knobs().wconv <= 0 || knobs().wconv3 == 0) return false;
   const alcm_opconv_args& a0 = a[0];
-  if ((a0.prec != PREC_F16 && a0.prec != PREC_BF16) || !a0.out || a0.Cp % 64 || a0.N % W3_BN) return 0;
+  if ((a0.prec != PREC_F16 && a0.prec != PREC_BF16) || a0.Cp % 64 || a0.N % W3_BN) return false;
+  // output: fp32 out, or (no accumulate) the operand plane of the value the fp32 route would store
+  if (a0.out_plane ? (a0.out || a0.accumulate || (((uintptr_t)a0.out_plane) & 3)) : !a0.out) return false;
   for (int i = 0; i < n; ++i) {
     const alcm_opconv_args& t = a[i];
     if (t.B != a0.B || t.T != a0.T || t.Cp != a0.Cp || t.N != a0.N || t.prec != a0.prec || t.dil != 1 ||
         t.ksize < 3 || t.ksize - 1 > 64 || 2 * t.pad != t.ksize - 1 || t.out_act || t.out_stride > 0 ||
-        t.geglu_plane || t.out_plane || t.act_plane || (int64_t)W3_BN * t.kpad * 2 >= (1ll << 31))
-      return 0;
+        t.geglu_plane || (i > 0 && t.out_plane) || t.act_plane || (int64_t)W3_BN * t.kpad * 2 >= (1ll << 31))
+      return false;
   }
   if (!g_ncu) {
     int dev = 0, nc = 0;
@@ -896,20 +936,27 @@ int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
   const int mt256 = (a0.T + W3_BM - 1) / W3_BM;
   const int64_t nt = (int64_t)a0.B * mt256 * (a0.N / W3_BN);
   const bool full = a0.T * 100 >= mt256 * W3_BM * 85;
-  if (!(knobs().wconv3 > 0 || (full && nt >= g_ncu))) return 0;
-  if (nt >= (1ll << 30) || (int64_t)a0.B * a0.T * a0.Cp >= (1ll << 40) || (int64_t)a0.B * a0.T * a0.N >= (1ll << 40))
-    return 0;
+  if (!(knobs().wconv3 > 0 || (full && nt >= g_ncu))) return false;
+  return nt < (1ll << 30) && (int64_t)a0.B * a0.T * a0.Cp < (1ll << 40) && (int64_t)a0.B * a0.T * a0.N < (1ll << 40);
+}
+
+int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
+  if (!wconv3_sum_ok(a, n)) return 0;  // (sets g_ncu)
+  const alcm_opconv_args& a0 = a[0];
+  const int mt256 = (a0.T + W3_BM - 1) / W3_BM;
+  const int64_t nt = (int64_t)a0.B * mt256 * (a0.N / W3_BN);
   WConvDev P{};
   P.a = (const u16*)a0.a;
   P.T = a0.T; P.Cp = a0.Cp; P.ksize = a0.ksize; P.dil = 1; P.pad = a0.pad;
   P.N = a0.N;
   P.out = a0.out; P.out_scale = a0.out_scale; P.accumulate = a0.accumulate;
+  P.oplane = (u16*)a0.out_plane;
   P.tiles_per_batch = mt256;
   P.tiles_n = a0.N / W3_BN;
   P.nwg = (int)nt;
   P.n_major = 1;
   P.nseg = n;
-  double flops = 0, bytes = (double)a0.B * a0.T * a0.N * 4.0 * (a0.accumulate ? 2 : 1);
+  double flops = 0, bytes = (double)a0.B * a0.T * a0.N * (a0.out_plane ? 2.0 : 4.0 * (a0.accumulate ? 2 : 1));
   for (int i = 0; i < n; ++i) {
     const bool f16 = a[i].prec == PREC_F16;
     P.sa[i] = (const u16*)a[i].a;

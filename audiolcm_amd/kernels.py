@@ -358,11 +358,13 @@ def activation1d_op_f16in(x16: torch.Tensor, alpha: torch.Tensor, beta: torch.Te
     return y
 
 
-def opconv_sum(terms, prec: int, out_scale: float = 1.0, accumulate_into: Optional[torch.Tensor] = None):
+def opconv_sum(terms, prec: int, out_scale: float = 1.0, accumulate_into: Optional[torch.Tensor] = None,
+               out_plane: bool = False):
     """alcm_opconv_sum: out (B, T, N) = (sum over terms of conv_k(planes) + bias + residual) * out_scale (+ out) — the
     mean over a BigVGAN stage's resblocks at their last conv2 + residual (vocoder/bigvgan/models.py:190-199).
     terms: up to three (planes (1, B, T, Cp), w (N, C, k), bias or None, residual (B, T, N) or None, packed or None),
-    same-length dilation-1 convs sharing B, T and N."""
+    same-length dilation-1 convs sharing B, T and N.  out_plane = True: the result as one PREC operand plane
+    (1, B, T, N) instead (the one-launch form only, no accumulate)."""
     n = len(terms)
     assert 1 <= n <= 3
     args = (_hip.OpConvArgs * n)()
@@ -390,6 +392,10 @@ def opconv_sum(terms, prec: int, out_scale: float = 1.0, accumulate_into: Option
         a.prec = int(prec)
         if i == 0:
             a.out, a.out_scale, a.accumulate = ptr(out), out_scale, int(accumulate_into is not None)
+            if out_plane:
+                assert accumulate_into is None
+                out = torch.empty((1, B, T, N), dtype=torch.int16, device=planes.device)
+                a.out, a.out_plane = None, ptr(out)
     check(lib().alcm_opconv_sum(args, n, stream_handle()), "opconv_sum")
     return out
 

@@ -970,3 +970,31 @@ def test_opconv_sum_three_chains(K, C, T, grid, acc, monkeypatch):
     e_ref, e_seq = rel_l2(outs[0].numpy(), ref.numpy()), rel_l2(outs[0].numpy(), outs[1].numpy())
     print(f"opconv_sum C{C} T{T}: vs F.conv1d {e_ref:.2e}, vs three launches {e_seq:.2e}")
     assert e_ref < 1e-5 and e_seq < 1e-6
+
+
+@pytest.mark.parametrize("C,T,grid", [(384, 1100, 0), (768, 600, 8)])
+def test_opconv_sum_plane_output(K, C, T, grid, monkeypatch):
+    """alcm_opconv_sum writing the stage output as the next stage's fp16 operand plane (its only consumer, the
+    upsampler's phase convs, vocoder/bigvgan/models.py:187-188, reads that format): bit for bit the fp16 rounding
+    (operand_planes) of the same launch's fp32 output, on the multi-tile walk too."""
+    from audiolcm_amd import _hip
+    B, inv = 2, 1.0 / 3
+    ks = (3, 7, 11)
+    terms = []
+    for i, k in enumerate(ks):
+        pl = K.operand_planes(dev(_r((B, T, C), 230 + i, 0.5)), 2)
+        w = dev(_r((C, C, k), 233 + i, 1.0 / np.sqrt(C * k)))
+        terms.append((pl, w, dev(_r((C,), 236 + i, 0.05)), dev(_r((B, T, C), 239 + i)), K.pack_conv_weight(w)))
+    monkeypatch.setenv("ALCM_WCONV3", "1")
+    monkeypatch.setenv("ALCM_WCONV3_GRID", str(grid))
+    _hip.reload_knobs()
+    try:
+        y32 = K.opconv_sum(terms, 2, out_scale=inv)
+        y16 = K.opconv_sum(terms, 2, out_scale=inv, out_plane=True)
+        ref16 = K.operand_planes(y32, 2)
+        torch.cuda.synchronize()
+    finally:
+        monkeypatch.delenv("ALCM_WCONV3")
+        monkeypatch.delenv("ALCM_WCONV3_GRID")
+        _hip.reload_knobs()
+    assert torch.equal(y16.cpu(), ref16.cpu()), "sum-form plane != fp16(fp32 sum output)"
