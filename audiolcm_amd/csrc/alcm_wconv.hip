@@ -898,8 +898,9 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   if (ks > 1) ksplit_reduce(a, ks, s);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), ks > 1 ? "alcm::wconv3_kernel<%d> + ksplit_reduce" : "alcm::wconv3_kernel<%d>",
-                  a.prec);
+    // (the rocprofv3 names of the instantiations, so bench.py finds their PMC traffic in profiles/*/kernels.json)
+    std::snprintf(name, sizeof(name),
+                  ks > 1 ? "alcm::wconv3_kernel<%d, 1> + ksplit_reduce" : "alcm::wconv3_kernel<%d, 1>", a.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -979,7 +980,7 @@ int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
   else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 3>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, sum3>", a0.prec);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 3>", a0.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d+%d+%d", a0.T, a0.Cp,
                     a0.N, a[0].ksize, a[1].ksize, a[2].ksize);

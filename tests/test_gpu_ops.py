@@ -961,8 +961,8 @@ def test_opconv_sum_three_chains(K, C, T, grid, acc, monkeypatch):
             for kk in env:
                 monkeypatch.delenv(kk)
             _hip.reload_knobs()
-    assert any("sum3" in n for n in names[0]), names[0]
-    assert not any("sum3" in n for n in names[1]), names[1]
+    assert any("wconv3_kernel<2, 3>" in n for n in names[0]), names[0]
+    assert not any("wconv3_kernel<2, 3>" in n for n in names[1]), names[1]
     ref = sum(F.conv1d(xs[i].half().float().permute(0, 2, 1), ws[i].half().float(), bs[i],
                        padding=(ks[i] - 1) // 2).permute(0, 2, 1) + rs[i] for i in range(3)) * inv
     if acc:
