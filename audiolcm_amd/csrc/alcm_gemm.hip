@@ -403,6 +403,121 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
   }
 }
 
+// ---------------------------------------------------------------- skinny GEMM (M <= 64 rows, k = 1)
+// The DiT embedder MLPs run at M = B rows (concatDiT.py TimestepEmbedder / proj_w: Linear -> SiLU -> Linear): on the
+// MFMA tiles a 32-row problem is 1-5 workgroups walking K serially (45 us a launch, latency-bound).  Here a
+// workgroup owns 32 output columns and every row: A (M x Kpad fp32, zero past C_in) staged once in LDS, 256 threads =
+// 32 columns x 8 K slices, fp32 FMAs of the A element (rounded to the operand format for BF16 / F16 like the MFMA
+// path; SPLIT keeps fp32) with the weight's value in that format (SPLIT: bf16 hi + lo), the slices' partials added in
+// slice order, then the MFMA kernels' epilogue (acc_scale, bias, act, residual, out_scale, accumulate).
+constexpr int SK_N = 32, SK_LDS = 24576;  // columns per workgroup; LDS floats (M * Kpad <= SK_LDS)
+template <int PREC>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
+  __shared__ __attribute__((aligned(16))) float sm[SK_LDS];
+  const int tid = threadIdx.x, c = tid & 31, ks = tid >> 5;
+  const int n = blockIdx.x * SK_N + c;
+  const int M = P.M, K = P.Kpad;
+  const ActDev& A = P.a;
+  // A staged as float4 pieces (rows channel-contiguous, C_in % 4 == 0: checked by the host), eight loads in flight per
+  // thread before their stores (one at a time, each store waited on its load: 72 serialised L2 trips a launch)
+  const int K4 = K >> 2, n4 = M * K4;
+  for (int e0 = tid; e0 < n4; e0 += 256 * 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 256;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < n4) {
+        const int m = e / K4, k = (e - m * K4) * 4;
+        if (k < A.C_in) {
+          uint32_t b, t;
+          A.rpb.divmod((uint32_t)m, b, t);
+          v[u] = *reinterpret_cast<const float4*>(A.p + (int64_t)b * A.sb + (int64_t)t * A.st + k);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 256;
+      if (e >= n4) continue;
+      float4 x = v[u];
+      if constexpr (PREC == PREC_F16) {
+        x.x = (float)(_Float16)x.x; x.y = (float)(_Float16)x.y; x.z = (float)(_Float16)x.z; x.w = (float)(_Float16)x.w;
+      }
+      if constexpr (PREC == PREC_BF16) {
+        x.x = (float)(__bf16)x.x; x.y = (float)(__bf16)x.y; x.z = (float)(__bf16)x.z; x.w = (float)(__bf16)x.w;
+      }
+      *reinterpret_cast<float4*>(sm + 4 * e) = x;
+    }
+  }
+  __syncthreads();
+  float acc[64];
+#pragma unroll
+  for (int m = 0; m < 64; ++m) acc[m] = 0.f;
+  const bool nok = n < P.N;
+  // the weight pieces one K step ahead (the next step's loads in flight under this step's FMAs)
+  const u16* wrow = P.w.p + (int64_t)(nok ? n : 0) * K;
+  bf16x8 hn = {}, ln = {};
+  if (nok && 8 * ks < K) {
+    hn = *reinterpret_cast<const bf16x8*>(wrow + 8 * ks);
+    if constexpr (PREC == PREC_SPLIT) ln = *reinterpret_cast<const bf16x8*>(wrow + P.w.lo + 8 * ks);
+  }
+  for (int k0 = 8 * ks; k0 < K; k0 += 64) {
+    const bf16x8 h = hn, l = ln;
+    if (nok && k0 + 64 < K) {
+      hn = *reinterpret_cast<const bf16x8*>(wrow + k0 + 64);
+      if constexpr (PREC == PREC_SPLIT) ln = *reinterpret_cast<const bf16x8*>(wrow + P.w.lo + k0 + 64);
+    }
+    float w[8];
+    if constexpr (PREC == PREC_F16) {
+      const f16x8 hf = __builtin_bit_cast(f16x8, h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = (float)hf[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = (float)h[j];
+      if constexpr (PREC == PREC_SPLIT) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] += (float)l[j];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      if (m < M) {
+        const float4 a0 = *reinterpret_cast<const float4*>(sm + m * K + k0);
+        const float4 a1 = *reinterpret_cast<const float4*>(sm + m * K + k0 + 4);
+        float v = acc[m];
+        v = fmaf(a0.x, w[0], v); v = fmaf(a0.y, w[1], v); v = fmaf(a0.z, w[2], v); v = fmaf(a0.w, w[3], v);
+        v = fmaf(a1.x, w[4], v); v = fmaf(a1.y, w[5], v); v = fmaf(a1.z, w[6], v); v = fmaf(a1.w, w[7], v);
+        acc[m] = v;
+      }
+    }
+  }
+  __syncthreads();  // every A read done: the buffer takes the 8 slices' partials [slice][row][column]
+#pragma unroll
+  for (int m = 0; m < 64; ++m)
+    if (m < M) sm[(ks * 64 + m) * SK_N + c] = acc[m];
+  __syncthreads();
+  const EpiDev& E = P.e;
+  for (int m = ks; m < M; m += 8) {
+    float v = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) v += sm[(s2 * 64 + m) * SK_N + c];
+    if (!nok) continue;
+    uint32_t bb = 0, tt = 0;
+    E.orpb.divmod((uint32_t)m, bb, tt);
+    const int64_t to = (int64_t)tt * E.out_step + E.out_off;
+    v *= E.acc_scale;
+    if (E.bias) v += E.bias[n];
+    if (E.act) v = alcm_act(v, E.act);
+    if (E.res) v += E.res[(int64_t)bb * E.r_sb + to * E.r_st + (int64_t)n * E.r_sc];
+    v *= E.out_scale;
+    float* o = E.out + (int64_t)bb * E.o_sb + to * E.o_st + (int64_t)n * E.o_sc;
+    if (E.accumulate) v += *o;
+    *o = v;
+  }
+}
+
 // ---------------------------------------------------------------- window convolution (ksize > 1)
 // Implicit GEMM for conv1d with k taps where the A operand of every tap is a shifted view of
 // one input window: for each 32-channel chunk the rows [t0 - pad, t0 + BM + (k-1)*dil - pad)
@@ -761,8 +876,30 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
       if (pro) launch_conv_sp<128, 128, 2, 2, true>(P, nb, T_out, split, s);
       else launch_conv_sp<128, 128, 2, 2, false>(P, nb, T_out, split, s);
     }
+  } else if (bkind == BK_W && batch == 1 && g.M <= 64 && g.a.ksize == 1 && P.a.pad == 0 && P.a.up != 2 &&
+             !P.a.pm && !P.a.ps && !P.a.pact && !g.geglu && (int64_t)g.M * g.Kpad <= SK_LDS && g.Kpad % 8 == 0 &&
+             g.a.sc == 1 && g.a.C_in % 4 == 0 && g.a.st % 4 == 0 && g.a.sb % 4 == 0 && (((uintptr_t)g.a.ptr) & 15) == 0 &&
+             knobs().gemm_skinny) {
+    // the embedder MLPs' M = B rows (gemm_skinny_kernel)
+    const unsigned grid = (unsigned)((N + SK_N - 1) / SK_N);
+    void* tok = prof_start(s);
+    if (split == PREC_SPLIT) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_SPLIT>), dim3(grid), dim3(256), 0, s, P);
+    else if (split == PREC_F16) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_F16>), dim3(grid), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<PREC_BF16>), dim3(grid), dim3(256), 0, s, P);
+    if (tok) {
+      char name[96];
+      std::snprintf(name, sizeof(name), "alcm::gemm_skinny_kernel<%d>", split);
+      if (knobs().prof_shapes)
+        std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " M%d N%d K%d", g.M, N, g.Kpad);
+      prof_stop(tok, s, name, g_cost.flops, g_cost.bytes);
+    }
   } else if (bkind == BK_W) {
-    if (N <= 32) {
+    // (N <= 32 on fewer than 128 tiles of 256 rows: 64-row tiles, 4x the workgroups — the DiT final layer, M = B T rows
+    // x N = 20: 39 -> 156 workgroups; the same K order per output, bit-identical)
+    if (N <= 32 && (int64_t)((g.M + 255) / 256) * batch < 128 && knobs().gemm_skinny) {
+      if (avec) launch_split<64, 32, 4, 1, true, BK_W>(P, batch, N, split, s);
+      else launch_split<64, 32, 4, 1, false, BK_W>(P, batch, N, split, s);
+    } else if (N <= 32) {
       if (avec) launch_split<256, 32, 4, 1, true, BK_W>(P, batch, N, split, s);
       else launch_split<256, 32, 4, 1, false, BK_W>(P, batch, N, split, s);
     } else if (N <= 64) {

@@ -130,6 +130,8 @@ struct Knobs {
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
   int act_x3_mfma = 1;           // ALCM_ACT_X3_MFMA: the wide stages' three first Activation1d in one MFMA-FIR pass (0 = three)
+  int ups_t160 = 1;              // ALCM_UPS_T160: strided (upsampler phase) wconv2 launches may take 160-row tiles
+  int gemm_skinny = 1;           // ALCM_GEMM_SKINNY: M <= 64-row k = 1 GEMMs on gemm_skinny_kernel (0 = MFMA tiles)
   int wconv_sum = 1;             // ALCM_WCONV_SUM: the wide stages' three chains' last conv2 + residual in one sum-form
                                  // launch writing the next stage's upsampler planes (2 = fp32 output + to_planes,
                                  // 0 = three accumulating launches)

@@ -38,6 +38,8 @@ static Knobs read_knobs() {
   k.ksplit = env_int("ALCM_KSPLIT", 1);
   k.act_x3_mfma = env_int("ALCM_ACT_X3_MFMA", 1);
   k.wconv_sum = env_int("ALCM_WCONV_SUM", 1);
+  k.gemm_skinny = env_int("ALCM_GEMM_SKINNY", 1);
+  k.ups_t160 = env_int("ALCM_UPS_T160", 1);
   return k;
 }
 

@@ -379,7 +379,8 @@ template <typename V>
 __device__ __forceinline__ V w3_sel(const V (&v)[3], int i) {
   return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
 }
-template <int PREC, int SEG>
+// KSP: the K-split form (P.ksplit parts) is compiled in (its own instantiation, so profiles tell the two apart)
+template <int PREC, int SEG, bool KSP>
 __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   constexpr int TM = 4, TN = 6;
   __shared__ __attribute__((aligned(1024))) char smem[2 * W3_WBUF + 3 * W3_BBUF];
@@ -390,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void wconv3_kernel(const WConvDev P) {
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   // work items: tiles, or (K split) (part, tile) pairs part-major, so an XCD's contiguous item range walks the
   // tiles of one part as the unsplit kernel walks its tiles
-  const int KS = P.ksplit > 1 ? P.ksplit : 1;
+  const int KS = KSP && P.ksplit > 1 ? P.ksplit : 1;
   const int ntiles = P.nwg;
   const int nitems = ntiles * KS;
   const int R = (nitems + 7) >> 3;
@@ -893,14 +894,20 @@ static int wconv3_try(const alcm_opconv_args& a, const u16* wplane, double flops
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  if (a.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1>), dim3(grid), dim3(512), 0, s, P);
-  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 1>), dim3(grid), dim3(512), 0, s, P);
+  if (a.prec == PREC_F16) {
+    if (ks > 1) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1, true>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 1, false>), dim3(grid), dim3(512), 0, s, P);
+  } else {
+    if (ks > 1) hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 1, true>), dim3(grid), dim3(512), 0, s, P);
+    else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 1, false>), dim3(grid), dim3(512), 0, s, P);
+  }
   if (ks > 1) ksplit_reduce(a, ks, s);
   if (tok) {
     char name[96];
     // (the rocprofv3 names of the instantiations, so bench.py finds their PMC traffic in profiles/*/kernels.json)
     std::snprintf(name, sizeof(name),
-                  ks > 1 ? "alcm::wconv3_kernel<%d, 1> + ksplit_reduce" : "alcm::wconv3_kernel<%d, 1>", a.prec);
+                  ks > 1 ? "alcm::wconv3_kernel<%d, 1, true> + ksplit_reduce" : "alcm::wconv3_kernel<%d, 1, false>",
+                  a.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d", a.T, a.Cp, a.N,
                     a.ksize);
@@ -976,11 +983,11 @@ int wconv3_sum_try(const alcm_opconv_args* a, int n, hipStream_t s) {
   int grid = 8 * std::min(g_ncu / 8, R);
   if (knobs().wconv3_grid >= 8) grid = std::min(grid, knobs().wconv3_grid / 8 * 8);  // tests: several tiles per workgroup
   void* tok = prof_start(s);
-  if (a0.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 3>), dim3(grid), dim3(512), 0, s, P);
-  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 3>), dim3(grid), dim3(512), 0, s, P);
+  if (a0.prec == PREC_F16) hipLaunchKernelGGL((wconv3_kernel<PREC_F16, 3, false>), dim3(grid), dim3(512), 0, s, P);
+  else hipLaunchKernelGGL((wconv3_kernel<PREC_BF16, 3, false>), dim3(grid), dim3(512), 0, s, P);
   if (tok) {
     char name[96];
-    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 3>", a0.prec);
+    std::snprintf(name, sizeof(name), "alcm::wconv3_kernel<%d, 3, false>", a0.prec);
     if (knobs().prof_shapes)
       std::snprintf(name + std::strlen(name), sizeof(name) - std::strlen(name), " T%d C%d N%d k%d+%d+%d", a0.T, a0.Cp,
                     a0.N, a[0].ksize, a[1].ksize, a[2].ksize);
@@ -1049,8 +1056,10 @@ int wconv_try(const alcm_opconv_args& a, const u16* wplane, double flops, double
   // 160-row tiles where rounds x tile rows over the two-workgroup slots of the chip drop: the VAE's T = 312 k3 convs at
   // N = 1536 (768 tiles of 128 rows = 1.5 rounds, 512 of 160 = one; 1.82 -> 1.43 ms/step); N = 768
   // (384 tiles, one round either way) stays at 128
+  // (strided: the BigVGAN stage 0 / 1 upsampler phases, T = 624 / 2496 at N = 768 / 384: 1.25 / 2.5 rounds of
+  // 128-row tiles -> one / two of 160-row ones; ALCM_UPS_T160=0 keeps them at 128)
   bool t160 = false;
-  if (!t256 && !a.geglu_plane && !strided && a.N % 192 == 0) {
+  if (!t256 && !a.geglu_plane && (!strided || knobs().ups_t160) && a.N % 192 == 0) {
     const int64_t slots = 2 * (int64_t)g_ncu, tn = a.N / 192;
     const int64_t r128 = ((int64_t)a.B * ((a.T + 127) / 128) * tn + slots - 1) / slots;
     const int64_t r160 = ((int64_t)a.B * ((a.T + 159) / 160) * tn + slots - 1) / slots;

@@ -961,8 +961,8 @@ def test_opconv_sum_three_chains(K, C, T, grid, acc, monkeypatch):
             for kk in env:
                 monkeypatch.delenv(kk)
             _hip.reload_knobs()
-    assert any("wconv3_kernel<2, 3>" in n for n in names[0]), names[0]
-    assert not any("wconv3_kernel<2, 3>" in n for n in names[1]), names[1]
+    assert any("wconv3_kernel<2, 3, false>" in n for n in names[0]), names[0]
+    assert not any("wconv3_kernel<2, 3, false>" in n for n in names[1]), names[1]
     ref = sum(F.conv1d(xs[i].half().float().permute(0, 2, 1), ws[i].half().float(), bs[i],
                        padding=(ks[i] - 1) // 2).permute(0, 2, 1) + rs[i] for i in range(3)) * inv
     if acc:
@@ -998,3 +998,103 @@ def test_opconv_sum_plane_output(K, C, T, grid, monkeypatch):
         monkeypatch.delenv("ALCM_WCONV3_GRID")
         _hip.reload_knobs()
     assert torch.equal(y16.cpu(), ref16.cpu()), "sum-form plane != fp16(fp32 sum output)"
+
+
+@pytest.mark.parametrize("M,K_,N,act,res,split", [(32, 256, 576, 1, False, True), (32, 576, 576, 0, True, True),
+                                                (20, 96, 200, 0, True, True), (64, 256, 256, 1, False, False)])
+def test_gemm_skinny_rows(K, M, K_, N, act, res, split, monkeypatch):
+    """gemm_skinny_kernel: the DiT embedder MLPs at M = B rows (concatDiT.py TimestepEmbedder: Linear -> SiLU ->
+    Linear, + residual) on fp32 FMAs of the operand-format values vs F.linear (fp32) and vs the MFMA tiles
+    (ALCM_GEMM_SKINNY=0); the split form uses the weight's hi + lo value and the fp32 activation."""
+    from audiolcm_amd import _hip
+    x = _r((1, M, K_), 240, 0.5)
+    w, b = _r((N, K_, 1), 241, 1.0 / np.sqrt(K_)), _r((N,), 242, 0.05)
+    r = _r((1, M, N), 243) if res else None
+    ref = F.linear(x, w[..., 0], b)
+    if act:
+        ref = F.silu(ref)
+    if res:
+        ref = ref + r
+    outs, names = [], []
+    for sk in ("1", "0"):
+        monkeypatch.setenv("ALCM_GEMM_SKINNY", sk)
+        _hip.reload_knobs()
+        try:
+            _hip.profile_begin()
+            y = K.conv1d(dev(x), dev(w), dev(b), channels_last=True, act=act,
+                         residual=dev(r) if res else None, split=split)
+            torch.cuda.synchronize()
+            names.append([p["name"] for p in _hip.profile_end()])
+            outs.append(y.cpu())
+        finally:
+            monkeypatch.delenv("ALCM_GEMM_SKINNY")
+            _hip.reload_knobs()
+    assert any("skinny" in n for n in names[0]) and not any("skinny" in n for n in names[1]), names
+    # (split: the weight's hi + lo value carries ~2^-17 relative error per weight, on both paths)
+    tol = 1e-5 if split else 1e-2
+    e_ref, e_mfma = rel_l2(outs[0].numpy(), ref.numpy()), rel_l2(outs[0].numpy(), outs[1].numpy())
+    print(f"skinny M{M} K{K_} N{N}: vs F.linear {e_ref:.2e}, vs MFMA tiles {e_mfma:.2e}")
+    assert e_ref < tol and e_mfma < 2 * tol
+
+
+def test_gemm_narrow_n_small_tiles(K, monkeypatch):
+    """The DiT final layer shape class (N = 20 output channels over B T rows, concatDiT.py FinalLayer linear) on
+    64-row MFMA tiles (4x the workgroups of the 256-row tiles): the same K order per output, so bit-identical to the
+    256-row tiles (ALCM_GEMM_SKINNY=0), and vs F.linear within the split bound."""
+    from audiolcm_amd import _hip
+    M, K_, N = 2000, 576, 20
+    x = _r((1, M, K_), 250, 0.5)
+    w, b = _r((N, K_, 1), 251, 1.0 / np.sqrt(K_)), _r((N,), 252, 0.05)
+    outs = []
+    for sk in ("1", "0"):
+        monkeypatch.setenv("ALCM_GEMM_SKINNY", sk)
+        monkeypatch.setenv("ALCM_PROF_SHAPES", "1")
+        _hip.reload_knobs()
+        try:
+            _hip.profile_begin()
+            outs.append(K.conv1d(dev(x), dev(w), dev(b), channels_last=True).cpu())
+            torch.cuda.synchronize()
+            names = [p["name"] for p in _hip.profile_end()]
+        finally:
+            monkeypatch.delenv("ALCM_GEMM_SKINNY")
+            monkeypatch.delenv("ALCM_PROF_SHAPES")
+            _hip.reload_knobs()
+        assert any(("gemm_kernel<64, 32" if sk == "1" else "gemm_kernel<256, 32") in n for n in names), names
+    assert torch.equal(outs[0], outs[1])
+    assert rel_l2(outs[0].numpy(), F.linear(x, w[..., 0], b).numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("Cin,N,T,rate", [(1536, 768, 624, 4), (768, 384, 2496, 4)])
+def test_strided_upsampler_160_row_tiles(K, Cin, N, T, rate, monkeypatch):
+    """The BigVGAN stage 0 / 1 upsampler phases at the bench batch (B = 32; models.py:160-165 ConvTranspose1d as
+    phase convs with the strided epilogue) on 160-row wconv2 tiles: the same K order per output as the 128-row
+    tiles (ALCM_UPS_T160=0, checked against torch's conv_transpose1d in test_opconv_strided_convtranspose), so
+    bit-identical; the profile shows the 160-row instantiation ran."""
+    from audiolcm_amd import _hip
+    B, k, prec = 32, 2 * rate, 2
+    x = _r((B, T, Cin), 260, 0.5)
+    w, bias = _r((Cin, N, k), 261, 1.0 / np.sqrt(Cin * 2)), _r((N,), 262, 0.05)
+    pl = K.operand_planes(dev(x), prec)
+    pad, Q = rate // 2, 2
+    shape_only = dev(torch.zeros((N, Cin, Q)))
+    pws = [K.pack_conv_weight(dev(w), transposed=True, stride=rate, phase=r) for r in range(rate)]
+    outs = []
+    for t160 in ("1", "0"):
+        monkeypatch.setenv("ALCM_UPS_T160", t160)
+        _hip.reload_knobs()
+        try:
+            _hip.profile_begin()
+            out = dev(torch.full((B, T * rate, N), float("nan")))
+            for r in range(rate):
+                o = (r - pad) % rate
+                c = (o + pad - r) // rate
+                K.opconv(pl, Cin, shape_only, dev(bias), 1, prec, packed=pws[r], strided=(out, rate, o, Q - 1 - c))
+            torch.cuda.synchronize()
+            names = [p["name"] for p in _hip.profile_end()]
+            outs.append(out.cpu())
+        finally:
+            monkeypatch.delenv("ALCM_UPS_T160")
+            _hip.reload_knobs()
+        assert any(("160, 192" if t160 == "1" else "128, 192") in n for n in names), names
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
