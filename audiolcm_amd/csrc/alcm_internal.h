@@ -45,6 +45,7 @@ int activation1d(const float* x, float* y, int B, int T, int C, int64_t sb, int6
 int lcm_step(const float* x, const float* eps, const float* eps_u, float cfg, const float* noise,
              const float* coeffs, float* prev, float* den, int64_t n, hipStream_t s);
 int fill_f32(float* p, int64_t n, float v, hipStream_t s);
+int nct_to_cl(const float* x, int B, int C, int T, int Cp, float* y, hipStream_t s);
 // fp32 rows [rows][C] -> operand planes [rows][Cp] in the format of `prec` (SPLIT: lo plane rows * Cp after hi)
 int to_planes(const float* x, void* y, int64_t rows, int C, int Cp, int prec, hipStream_t s);
 // BigVGAN output head: Activation1d -> conv_post (k7, C -> 1, weights [tap][C] fp32) -> tanh, fp32 (alcm_act.hip)
@@ -130,6 +131,8 @@ struct Knobs {
   int act_mfma = 1;              // ALCM_ACT_MFMA: Activation1d FIRs on MFMA for the wide stages (0 = VALU act_coop)
   int conv1_h16 = 1;             // ALCM_CONV1_H16: wide-stage AMPBlock conv1 writes an fp16 plane for its Activation1d
   int act_x3_mfma = 1;           // ALCM_ACT_X3_MFMA: the wide stages' three first Activation1d in one MFMA-FIR pass (0 = three)
+  int nct_cl = 1;                // ALCM_NCT_CL: NCT conv inputs (DiT proj_in, BigVGAN conv_pre) transposed to channels-last
+                                 // first (0 = strided gather in the conv)
   int ups_t160 = 1;              // ALCM_UPS_T160: strided (upsampler phase) wconv2 launches may take 160-row tiles
   int gemm_skinny = 1;           // ALCM_GEMM_SKINNY: M <= 64-row k = 1 GEMMs on gemm_skinny_kernel (0 = MFMA tiles)
   int wconv_sum = 1;             // ALCM_WCONV_SUM: the wide stages' three chains' last conv2 + residual in one sum-form

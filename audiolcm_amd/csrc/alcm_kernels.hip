@@ -494,6 +494,34 @@ int fill_f32(float* p, int64_t n, float v, hipStream_t s) {
   return 0;
 }
 
+// NCT (B, C, T) -> channels-last (B, T, Cp), channels C .. Cp - 1 zero: the reference-layout inputs of the DiT proj_in
+// and BigVGAN conv_pre (concatDiT.py proj_in on the NCT latent, models.py:183 on the NCT mel) as the vectorised
+// channel-contiguous operand of the implicit-GEMM conv instead of a stride-T gather per element.  32 x 32 tiles
+// through LDS (reads coalesced along t, writes along c).
+__global__ __launch_bounds__(256) void nct_to_cl_kernel(const float* __restrict__ x, int C, int T, int Cp,
+                                                        float* __restrict__ y) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + ty + 8 * j, t = t0 + tx;
+    tile[ty + 8 * j][tx] = (c < C && t < T) ? x[((int64_t)b * C + c) * T + t] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = t0 + ty + 8 * j, c = c0 + tx;
+    if (t < T && c < Cp) y[((int64_t)b * T + t) * Cp + c] = tile[tx][ty + 8 * j];
+  }
+}
+int nct_to_cl(const float* x, int B, int C, int T, int Cp, float* y, hipStream_t s) {
+  if (!x || !y || B <= 0 || C <= 0 || T <= 0 || Cp < C) return set_error(ALCM_E_INVALID, "nct_to_cl: bad arguments");
+  hipLaunchKernelGGL(nct_to_cl_kernel, dim3((T + 31) / 32, (Cp + 31) / 32, B), dim3(256), 0, s, x, C, T, Cp, y);
+  ALCM_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace alcm
 
 // ---------------------------------------------------------------- C-ABI

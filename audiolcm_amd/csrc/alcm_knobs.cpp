@@ -40,6 +40,7 @@ static Knobs read_knobs() {
   k.wconv_sum = env_int("ALCM_WCONV_SUM", 1);
   k.gemm_skinny = env_int("ALCM_GEMM_SKINNY", 1);
   k.ups_t160 = env_int("ALCM_UPS_T160", 1);
+  k.nct_cl = env_int("ALCM_NCT_CL", 1);
   return k;
 }
 

@@ -661,7 +661,9 @@ static int conv(hipStream_t s, int split, int B, int rows_per_batch, const View&
   a.rows_per_batch = rows_per_batch;
   a.pro_scale = op.pro.scale; a.pro_shift = op.pro.shift; a.pro_sb = op.pro.sb;
   a.pro_mean = op.pro.mean; a.pro_rstd = op.pro.rstd; a.pro_act = op.pro.act;
-  if (x.C != w.w.cin) return set_error(ALCM_E_INVALID, "conv: input channels do not match weight");
+  // (x.C == cpad > cin: a channels-last copy whose padding channels the caller zeroed, read as whole vectors)
+  if (x.C != w.w.cin && !(x.C == w.w.cpad && x.sc == 1))
+    return set_error(ALCM_E_INVALID, "conv: input channels do not match weight");
   alcm_operand& b = g.b;
   b.kind = ALCM_OPND_WEIGHT;
   b.ptr = w.w.p;
@@ -826,7 +828,15 @@ static int dit_forward(alcm_model* m, const float* x, const int64_t* t, const fl
     ConvOpts o;
     o.pad = D.pin_k / 2;
     o.res = Res{D.pos, 0, H, 1};
+    // the NCT latent as channels-last rows of cpad channels (zero padded) in w.o (free until the first block), so
+    // the conv reads whole vectors instead of a stride-T gather per element (ALCM_NCT_CL=0: the gather)
+    const int cp = D.proj_in.w.cpad;
+    const bool tcl = knobs().nct_cl && cp % 4 == 0 && (size_t)B * T * cp <= (size_t)B * L * H;
     View xv{x, (int64_t)D.in_ch * T, 1, T, T, D.in_ch};
+    if (tcl) {
+      ALCM_TRY(nct_to_cl(x, B, D.in_ch, T, cp, w.o, s));
+      xv = View{w.o, (int64_t)T * cp, cp, 1, T, cp};
+    }
     ALCM_TRY(conv(s, split, B, T, xv, D.proj_in, Out{w.h, (int64_t)L * H, H, 1, 1, E}, o));
   }
   const View hv = cl(w.h, L, H), uv = cl(w.u, L, H), ov = cl(w.o, L, H);
@@ -1072,16 +1082,23 @@ static int vae_decode(alcm_model* m, const float* z, float inv_scale, float* mel
   // z / scale_factor -> post_quant_conv (lcm_audio.py:403, autoencoder1d.py:59-62), z read as NCT
   ALCM_TRY(fill_f32(w.pqs, V.z_ch, inv_scale, s));
   ALCM_TRY(fill_f32(w.pqh, V.z_ch, 0.f, s));
+  // (post_quant_conv's rows written at conv_in's padded channel stride, the padding zeroed first: conv_in then reads
+  // whole vectors (ALCM_NCT_CL=0: rows of z_ch channels, read element by element))
+  const int cpi = V.conv_in.w.cpad;
+  const bool padrows = knobs().nct_cl && cpi > V.z_ch && cpi % 4 == 0;
+  const int dst = padrows ? cpi : V.z_ch;
+  if (padrows) ALCM_TRY(fill_f32(w.d, (int64_t)B * T * cpi, 0.f, s));
   {
     ConvOpts o;
     o.pro = Pro{w.pqs, w.pqh, 0, nullptr, nullptr, 0};
-    ALCM_TRY(conv(s, split, B, T, View{z, (int64_t)V.embed * T, 1, T, T, V.embed}, V.pqc, ocl(w.d, T, V.z_ch), o));
+    ALCM_TRY(conv(s, split, B, T, View{z, (int64_t)V.embed * T, 1, T, T, V.embed}, V.pqc,
+                  Out{w.d, (int64_t)T * dst, dst, 1, 1, 0}, o));
   }
   int C = V.ch * V.mult.back();
   {
     ConvOpts o;
     o.pad = V.ksz / 2;
-    ALCM_TRY(conv(s, split, B, T, cl(w.d, T, V.z_ch), V.conv_in, ocl(w.a, T, C), o));
+    ALCM_TRY(conv(s, split, B, T, View{w.d, (int64_t)T * dst, dst, 1, T, dst}, V.conv_in, ocl(w.a, T, C), o));
   }
   float* h = w.a;
   ALCM_TRY(vae_res(s, split, pk3, B, T, V.mid1, h, w.b, nullptr, h, w));
@@ -1425,8 +1442,15 @@ static int bigvgan_forward(alcm_model* m, const float* mel, float* wav, int B, i
   {
     ConvOpts o;
     o.pad = 3;
-    ALCM_TRY(conv(s, split, B, M, View{mel, (int64_t)G.num_mels * M, 1, M, M, G.num_mels}, G.pre, ocl(w.x, M, G.c0),
-                  o));
+    // the NCT mel as channels-last rows (chain 1's fp32 scratch, free until the first stage's chains), read as whole
+    // vectors instead of a stride-M gather per element (ALCM_NCT_CL=0: the gather)
+    const int cp = G.pre.w.cpad;
+    View mv{mel, (int64_t)G.num_mels * M, 1, M, M, G.num_mels};
+    if (knobs().nct_cl && cp % 4 == 0) {
+      ALCM_TRY(nct_to_cl(mel, B, G.num_mels, M, cp, w.ch[1].t, s));
+      mv = View{w.ch[1].t, (int64_t)M * cp, cp, 1, M, cp};
+    }
+    ALCM_TRY(conv(s, split, B, M, mv, G.pre, ocl(w.x, M, G.c0), o));
   }
   // buffer roles: x = stage input and (after the upsampler) stage output accumulator,
   // u = upsampler output (resblock input), rb = resblock running state, a / y = scratch
