@@ -546,7 +546,9 @@ static void build_voc(Ingest& I, const int* ic, int nic) {
     int nd = ic[p++];
     dil.assign(ic + p, ic + p + nd);
   }
-  G.pre.w = I.pack(I.wn("conv_pre.", {G.c0, G.num_mels, 7}), G.c0, G.num_mels, 7);
+  // (input channels padded to 32: the channels-last mel copy then takes the window conv, one staged window per
+  // 32-channel chunk shared by the 7 taps)
+  G.pre.w = I.pack(I.wn("conv_pre.", {G.c0, G.num_mels, 7}), G.c0, G.num_mels, 7, 0, 1, 0, 32);
   G.pre.b = I.upload(I.get("conv_pre.bias", {G.c0}));
   const int nk = (int)rk.size();
   for (size_t i = 0; i < rates.size(); ++i) {
