@@ -406,17 +406,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDev P) {
 // ---------------------------------------------------------------- skinny GEMM (M <= 64 rows, k = 1)
 // The DiT embedder MLPs run at M = B rows (concatDiT.py TimestepEmbedder / proj_w: Linear -> SiLU -> Linear): on the
 // MFMA tiles a 32-row problem is 1-5 workgroups walking K serially (45 us a launch, latency-bound).  Here a
-// workgroup owns 32 output columns and every row: A (M x Kpad fp32, zero past C_in) staged once in LDS, 256 threads =
+// workgroup owns 32 output columns x 32 rows: A (32 x Kpad fp32, zero past C_in) staged once in LDS, 256 threads =
 // 32 columns x 8 K slices, fp32 FMAs of the A element (rounded to the operand format for BF16 / F16 like the MFMA
 // path; SPLIT keeps fp32) with the weight's value in that format (SPLIT: bf16 hi + lo), the slices' partials added in
 // slice order, then the MFMA kernels' epilogue (acc_scale, bias, act, residual, out_scale, accumulate).
-constexpr int SK_N = 32, SK_LDS = 24576;  // columns per workgroup; LDS floats (M * Kpad <= SK_LDS)
+// Rows in blocks of SK_M (grid.y), so which rows share a launch never changes a row's arithmetic: the result is
+// invariant to how a batch is split (eligibility depends on K and the layer, not on M up to SK_MAXM rows).
+constexpr int SK_N = 32, SK_M = 32, SK_KMAX = 768, SK_MAXM = 1024;  // columns / rows per workgroup, K and M limits
 template <int PREC>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
-  __shared__ __attribute__((aligned(16))) float sm[SK_LDS];
+  __shared__ __attribute__((aligned(16))) float sm[SK_M * SK_KMAX];
   const int tid = threadIdx.x, c = tid & 31, ks = tid >> 5;
   const int n = blockIdx.x * SK_N + c;
-  const int M = P.M, K = P.Kpad;
+  const int m0 = blockIdx.y * SK_M;
+  const int M = min(P.M - m0, SK_M), K = P.Kpad;
   const ActDev& A = P.a;
   // A staged as float4 pieces (rows channel-contiguous, C_in % 4 == 0: checked by the host), eight loads in flight per
   // thread before their stores (one at a time, each store waited on its load: 72 serialised L2 trips a launch)
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
         const int m = e / K4, k = (e - m * K4) * 4;
         if (k < A.C_in) {
           uint32_t b, t;
-          A.rpb.divmod((uint32_t)m, b, t);
+          A.rpb.divmod((uint32_t)(m0 + m), b, t);
           v[u] = *reinterpret_cast<const float4*>(A.p + (int64_t)b * A.sb + (int64_t)t * A.st + k);
         }
       }
@@ -451,9 +454,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
     }
   }
   __syncthreads();
-  float acc[64];
+  float acc[SK_M];
 #pragma unroll
-  for (int m = 0; m < 64; ++m) acc[m] = 0.f;
+  for (int m = 0; m < SK_M; ++m) acc[m] = 0.f;
   const bool nok = n < P.N;
   // the weight pieces one K step ahead (the next step's loads in flight under this step's FMAs)
   const u16* wrow = P.w.p + (int64_t)(nok ? n : 0) * K;
@@ -482,7 +485,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
       }
     }
 #pragma unroll
-    for (int m = 0; m < 64; ++m) {
+    for (int m = 0; m < SK_M; ++m) {
       if (m < M) {
         const float4 a0 = *reinterpret_cast<const float4*>(sm + m * K + k0);
         const float4 a1 = *reinterpret_cast<const float4*>(sm + m * K + k0 + 4);
@@ -495,17 +498,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const GemmDev P) {
   }
   __syncthreads();  // every A read done: the buffer takes the 8 slices' partials [slice][row][column]
 #pragma unroll
-  for (int m = 0; m < 64; ++m)
-    if (m < M) sm[(ks * 64 + m) * SK_N + c] = acc[m];
+  for (int m = 0; m < SK_M; ++m)
+    if (m < M) sm[(ks * SK_M + m) * SK_N + c] = acc[m];
   __syncthreads();
   const EpiDev& E = P.e;
   for (int m = ks; m < M; m += 8) {
     float v = 0.f;
 #pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) v += sm[(s2 * 64 + m) * SK_N + c];
+    for (int s2 = 0; s2 < 8; ++s2) v += sm[(s2 * SK_M + m) * SK_N + c];
     if (!nok) continue;
     uint32_t bb = 0, tt = 0;
-    E.orpb.divmod((uint32_t)m, bb, tt);
+    E.orpb.divmod((uint32_t)(m0 + m), bb, tt);
     const int64_t to = (int64_t)tt * E.out_step + E.out_off;
     v *= E.acc_scale;
     if (E.bias) v += E.bias[n];
@@ -876,16 +879,16 @@ int gemm(const alcm_gemm_args& g, hipStream_t s) {
       if (pro) launch_conv_sp<128, 128, 2, 2, true>(P, nb, T_out, split, s);
       else launch_conv_sp<128, 128, 2, 2, false>(P, nb, T_out, split, s);
     }
-  } else if (bkind == BK_W && batch == 1 && g.M <= 64 && g.a.ksize == 1 && P.a.pad == 0 && P.a.up != 2 &&
-             !P.a.pm && !P.a.ps && !P.a.pact && !g.geglu && (int64_t)g.M * g.Kpad <= SK_LDS && g.Kpad % 8 == 0 &&
+  } else if (bkind == BK_W && batch == 1 && g.M <= SK_MAXM && g.a.ksize == 1 && P.a.pad == 0 && P.a.up != 2 &&
+             !P.a.pm && !P.a.ps && !P.a.pact && !g.geglu && g.Kpad <= SK_KMAX && g.Kpad % 8 == 0 &&
              g.a.sc == 1 && g.a.C_in % 4 == 0 && g.a.st % 4 == 0 && g.a.sb % 4 == 0 && (((uintptr_t)g.a.ptr) & 15) == 0 &&
              knobs().gemm_skinny) {
     // the embedder MLPs' M = B rows (gemm_skinny_kernel)
-    const unsigned grid = (unsigned)((N + SK_N - 1) / SK_N);
+    const dim3 grid((unsigned)((N + SK_N - 1) / SK_N), (unsigned)((g.M + SK_M - 1) / SK_M));
     void* tok = prof_start(s);
-    if (split == PREC_SPLIT) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_SPLIT>), dim3(grid), dim3(256), 0, s, P);
-    else if (split == PREC_F16) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_F16>), dim3(grid), dim3(256), 0, s, P);
-    else hipLaunchKernelGGL((gemm_skinny_kernel<PREC_BF16>), dim3(grid), dim3(256), 0, s, P);
+    if (split == PREC_SPLIT) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_SPLIT>), grid, dim3(256), 0, s, P);
+    else if (split == PREC_F16) hipLaunchKernelGGL((gemm_skinny_kernel<PREC_F16>), grid, dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<PREC_BF16>), grid, dim3(256), 0, s, P);
     if (tok) {
       char name[96];
       std::snprintf(name, sizeof(name), "alcm::gemm_skinny_kernel<%d>", split);

@@ -1098,3 +1098,15 @@ def test_strided_upsampler_160_row_tiles(K, Cin, N, T, rate, monkeypatch):
         assert any(("160, 192" if t160 == "1" else "128, 192") in n for n in names), names
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_gemm_skinny_batch_split_invariant(K):
+    """The skinny-row GEMM's rows are computed in fixed 32-row blocks and its eligibility does not depend on M (up to
+    1024 rows), so a batch split into shards gives bit-identical rows (bench.py's world-2 vs world-1 waveforms,
+    test_gpu_dist): 96 rows in one call == the same rows as 32 + 64."""
+    x = _r((1, 96, 576), 270, 0.5)
+    w, b = _r((576, 576, 1), 271, 1.0 / np.sqrt(576)), _r((576,), 272, 0.05)
+    full = K.conv1d(dev(x), dev(w), dev(b), channels_last=True, act=1).cpu()
+    a = K.conv1d(dev(x[:, :32].contiguous()), dev(w), dev(b), channels_last=True, act=1).cpu()
+    c = K.conv1d(dev(x[:, 32:].contiguous()), dev(w), dev(b), channels_last=True, act=1).cpu()
+    assert torch.equal(full, torch.cat([a, c], 1))
