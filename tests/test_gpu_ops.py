@@ -1110,3 +1110,25 @@ def test_gemm_skinny_batch_split_invariant(K):
     a = K.conv1d(dev(x[:, :32].contiguous()), dev(w), dev(b), channels_last=True, act=1).cpu()
     c = K.conv1d(dev(x[:, 32:].contiguous()), dev(w), dev(b), channels_last=True, act=1).cpu()
     assert torch.equal(full, torch.cat([a, c], 1))
+
+
+def test_opconv_sum_fallback_and_errors(K):
+    """alcm_opconv_sum outside the one-launch form: two terms (or shapes the persistent kernel does not take) run as
+    accumulating launches with the same result up to fp32 order (vs F.conv1d); a plane output there is an error, not a
+    silent fp32 write (include/audiolcm_hip.h)."""
+    from audiolcm_amd import _hip
+    B, T, C, inv = 2, 300, 192, 0.5
+    ks = (3, 5)
+    xs = [_r((B, T, C), 280 + i, 0.5) for i in range(2)]
+    ws = [_r((C, C, k), 282 + i, 1.0 / np.sqrt(C * k)) for i, k in enumerate(ks)]
+    bs = [_r((C,), 284 + i, 0.05) for i in range(2)]
+    rs = [_r((B, T, C), 286 + i) for i in range(2)]
+    terms = [(K.operand_planes(dev(xs[i]), 2), dev(ws[i]), dev(bs[i]), dev(rs[i]), None) for i in range(2)]
+    y = K.opconv_sum(terms, 2, out_scale=inv).cpu()
+    ref = sum(F.conv1d(xs[i].half().float().permute(0, 2, 1), ws[i].half().float(), bs[i],
+                       padding=(ks[i] - 1) // 2).permute(0, 2, 1) + rs[i] for i in range(2)) * inv
+    e = rel_l2(y.numpy(), ref.numpy())
+    print(f"opconv_sum two terms (accumulating launches): vs F.conv1d {e:.2e}")
+    assert e < 1e-5
+    with pytest.raises(RuntimeError):
+        K.opconv_sum(terms, 2, out_scale=inv, out_plane=True)
